@@ -1,0 +1,74 @@
+#!/usr/bin/env python
+"""GEMM microbenchmark: the hand-written MFMA kernel vs hipBLASLt (torch.mm) on the GPT-2 step
+shapes (M = B*T tokens).  Random N(0,1) operands (zero-filled operands inflate MFMA clocks).
+Prints one JSON line per shape."""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+from mingpt_distributed_amd.ops import gemm as G
+
+
+def timeit(fn, iters=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+    for s, e in ev:
+        s.record()
+        fn()
+        e.record()
+    torch.cuda.synchronize()
+    ts = sorted(s.elapsed_time(e) for s, e in ev)
+    return ts[len(ts) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tokens", type=int, default=16384)
+    ap.add_argument("--D", type=int, default=768)
+    ap.add_argument("--V", type=int, default=50257)
+    a = ap.parse_args()
+    M, D, V = a.tokens, a.D, a.V
+    Vp = (V + 127) // 128 * 128
+    r = lambda *s: torch.randn(*s, device="cuda").to(torch.bfloat16)
+    rows = []
+    for name, N, K in [("qkv", 3 * D, D), ("attn_proj", D, D), ("fc", 4 * D, D), ("mlp_proj", D, 4 * D),
+                       ("lm_head", V, D)]:
+        x, w = r(M, K), r(N, K)
+        ld = Vp if name == "lm_head" else None
+        t_mine = timeit(lambda: G.gemm_nt(x, w, ld=ld))
+        t_blas = timeit(lambda: torch.mm(x, w.t()))
+        rows.append(("fwd_nt", name, M, N, K, t_mine, t_blas))
+        # dgrad: dx[M,K] = dy[M,N] @ w[N,K]
+        dy = r(M, Vp if name == "lm_head" else N)
+        if name == "lm_head":
+            dy[:, V:] = 0
+        t_mine = timeit(lambda: G.gemm_nn(dy, w))
+        dyv = dy[:, :N] if name == "lm_head" else dy
+        t_blas = timeit(lambda: torch.mm(dyv, w))
+        rows.append(("dgrad_nn", name, M, K, N, t_mine, t_blas))
+        # wgrad: dw[N,K] += dy^T x
+        c = torch.zeros(N, K, device="cuda")
+        t_mine = timeit(lambda: G.gemm_tn_acc(dy, x, c, n_valid=N))
+        t_blas = timeit(lambda: torch.mm(dyv.t(), x))
+        rows.append(("wgrad_tn", name, N, K, M, t_mine, t_blas))
+    tot_m = tot_b = 0.0
+    for kind, name, m, n, k, tm, tb in rows:
+        fl = 2.0 * m * n * k
+        tot_m += tm
+        tot_b += tb
+        print(json.dumps({"kind": kind, "layer": name, "M": m, "N": n, "K": k, "mine_ms": round(tm, 4),
+                          "hipblaslt_ms": round(tb, 4), "mine_tflops": round(fl / tm / 1e9, 1),
+                          "hipblaslt_tflops": round(fl / tb / 1e9, 1), "speedup": round(tb / tm, 3)}),
+              flush=True)
+    print(json.dumps({"total_mine_ms": round(tot_m, 3), "total_hipblaslt_ms": round(tot_b, 3)}))
+
+
+if __name__ == "__main__":
+    main()

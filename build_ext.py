@@ -1,0 +1,121 @@
+#!/usr/bin/env python
+"""Build the gfx950 extension in-tree: ``mingpt_distributed_amd/_C.so``.
+
+Explicit ``hipcc --offload-arch=gfx950`` compiles (no hipify pass, no JIT cache):
+
+* each ``csrc/kernels/*.hip`` -> object with device code for gfx950 only,
+* ``csrc/bindings.cpp``       -> host object against the torch headers,
+* link against the HIP runtime *bundled with torch* (``torch/lib/libamdhip64.so``), so the
+  process holds exactly one HIP runtime and our kernels share torch's streams and allocator.
+
+Incremental: an object is rebuilt only when its source or any header is newer.
+Usage: ``python build_ext.py [--force] [-j N] [--tools]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "mingpt_distributed_amd")
+BUILD = os.path.join(ROOT, "build", "obj")
+ARCH = os.environ.get("MINGPT_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result",
+                "-I" + os.path.join(ROOT, "csrc", "include"), "-ffp-contract=fast"]
+
+
+def _torch_paths():
+    import torch
+    from torch.utils.cpp_extension import include_paths
+
+    tdir = os.path.dirname(torch.__file__)
+    return include_paths(), os.path.join(tdir, "lib"), int(torch._C._GLIBCXX_USE_CXX11_ABI)
+
+
+def _newer(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
+        raise RuntimeError(f"compile failed: {cmd[-1]}")
+    return r
+
+
+def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    headers = glob.glob(os.path.join(ROOT, "csrc", "include", "*.h"))
+    kernels = sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip")))
+    incs, tlib, abi = _torch_paths()
+    py_inc = sysconfig.get_paths()["include"]
+
+    jobs_list = []
+    objs = []
+    for src in kernels:
+        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _newer(obj, [src] + headers):
+            jobs_list.append([HIPCC, *COMMON_FLAGS, "-x", "hip", "-c", "-o", obj, src])
+    bsrc = os.path.join(ROOT, "csrc", "bindings.cpp")
+    bobj = os.path.join(BUILD, "bindings.o")
+    objs.append(bobj)
+    if force or _newer(bobj, [bsrc] + headers):
+        jobs_list.append([HIPCC, *COMMON_FLAGS, "-x", "hip", "-c", "-o", bobj,
+                          *["-I" + p for p in incs], "-I" + py_inc,
+                          f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C",
+                          "-DTORCH_API_INCLUDE_EXTENSION_H", "-D__HIP_PLATFORM_AMD__=1",
+                          "-DUSE_ROCM=1", bsrc])
+    if jobs_list:
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            futs = {ex.submit(_run, c): c[-1] for c in jobs_list}
+            for f in cf.as_completed(futs):
+                f.result()
+                if verbose:
+                    print(f"[build_ext] compiled {os.path.relpath(futs[f], ROOT)}", flush=True)
+    out = os.path.join(PKG, "_C.so")
+    if force or _newer(out, objs):
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out, *objs,
+              "-L" + tlib, "-Wl,-rpath," + tlib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
+              "-ltorch_hip", "-ltorch_python", "-lamdhip64"])
+        if verbose:
+            print(f"[build_ext] linked {os.path.relpath(out, ROOT)}", flush=True)
+    return out
+
+
+def build_tools(verbose: bool = True):
+    """Native tools (standalone executables against /opt/rocm HIP + RCCL)."""
+    outdir = os.path.join(ROOT, "build", "bin")
+    os.makedirs(outdir, exist_ok=True)
+    built = []
+    for src in sorted(glob.glob(os.path.join(ROOT, "tools", "*.cpp"))):
+        exe = os.path.join(outdir, os.path.splitext(os.path.basename(src))[0])
+        if _newer(exe, [src]):
+            _run([HIPCC, "-O2", "-std=c++17", f"--offload-arch={ARCH}", "-x", "hip", "-o", exe, src,
+                  "-I/opt/rocm/include", "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"])
+            if verbose:
+                print(f"[build_ext] built {os.path.relpath(exe, ROOT)}", flush=True)
+        built.append(exe)
+    return built
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 8))
+    ap.add_argument("--tools", action="store_true", help="also build tools/*.cpp executables")
+    a = ap.parse_args()
+    build(force=a.force, jobs=a.jobs)
+    if a.tools:
+        build_tools()

@@ -1,0 +1,290 @@
+// torch <-> gfx950 kernel bindings.  Every op validates shapes/dtypes on the host BEFORE
+// launching (a mis-shaped launch can fault the GPU for the whole node), then launches on the
+// caller's current HIP stream.  Built into mingpt_distributed_amd/_C.so by build_ext.py.
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+
+#include "kernels.h"
+
+namespace {
+
+using mg::bf16_t;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+using DevGuard = c10::hip::HIPGuardMasqueradingAsCUDA;
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_BF16(t) \
+  CHECK_DEV(t);       \
+  TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bf16")
+#define CHECK_F32(t) \
+  CHECK_DEV(t);      \
+  TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be fp32")
+#define CHECK_I64(t) \
+  CHECK_DEV(t);      \
+  TORCH_CHECK((t).scalar_type() == at::kLong, #t " must be int64")
+
+inline bf16_t* bp(const at::Tensor& t) { return reinterpret_cast<bf16_t*>(t.data_ptr()); }
+inline float* fp(const at::Tensor& t) { return t.data_ptr<float>(); }
+inline float* fp_opt(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr<float>() : nullptr;
+}
+inline bf16_t* bp_opt(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? reinterpret_cast<bf16_t*>(t->data_ptr()) : nullptr;
+}
+
+// ------------------------------------------------------------------------------- layernorm
+std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b,
+                                      double eps) {
+  CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(b); CHECK_CONTIG(x);
+  const int64_t D = x.size(-1), M = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && D <= 4096, "layernorm: D must be a multiple of 8 and <= 4096");
+  TORCH_CHECK(w.numel() == D && b.numel() == D, "layernorm: weight/bias size mismatch");
+  DevGuard g(x.device());
+  auto y = at::empty_like(x);
+  auto mean = at::empty({M}, x.options().dtype(at::kFloat));
+  auto rstd = at::empty({M}, x.options().dtype(at::kFloat));
+  mg::layernorm_fwd(bp(x), bp(w), bp(b), bp(y), fp(mean), fp(rstd), (int)M, (int)D, (float)eps,
+                    cur_stream());
+  return {y, mean, rstd};
+}
+
+at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                         const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& dw,
+                         const at::Tensor& db) {
+  CHECK_BF16(dy); CHECK_BF16(x); CHECK_BF16(w); CHECK_F32(mean); CHECK_F32(rstd);
+  CHECK_F32(dw); CHECK_F32(db); CHECK_CONTIG(dy); CHECK_CONTIG(x);
+  const int64_t D = x.size(-1), M = x.numel() / D;
+  TORCH_CHECK(dy.numel() == x.numel() && dw.numel() == D && db.numel() == D && mean.numel() == M,
+              "layernorm_bwd: shape mismatch");
+  DevGuard g(x.device());
+  auto dx = at::empty_like(x);
+  auto ws = at::empty({(int64_t)(mg::layernorm_bwd_workspace((int)M, (int)D) / 4)},
+                      x.options().dtype(at::kFloat));
+  mg::layernorm_bwd(bp(dy), bp(x), bp(w), fp(mean), fp(rstd), bp(dx), fp(dw), fp(db), fp(ws),
+                    (int)M, (int)D, cur_stream());
+  return dx;
+}
+
+// ------------------------------------------------------------------------------- embedding
+at::Tensor embedding_fwd(const at::Tensor& idx, const at::Tensor& wte, const at::Tensor& wpe,
+                         double p, int64_t seed) {
+  CHECK_I64(idx); CHECK_BF16(wte); CHECK_BF16(wpe); CHECK_CONTIG(idx);
+  CHECK_CONTIG(wte); CHECK_CONTIG(wpe);
+  TORCH_CHECK(idx.dim() == 2, "idx must be [B, T]");
+  const int64_t B = idx.size(0), T = idx.size(1), D = wte.size(1);
+  TORCH_CHECK(D % 8 == 0 && wpe.size(1) == D && T <= wpe.size(0), "embedding: shape mismatch");
+  DevGuard g(idx.device());
+  auto out = at::empty({B, T, D}, wte.options());
+  mg::embedding_fwd(idx.data_ptr<int64_t>(), bp(wte), bp(wpe), bp(out), (int)(B * T), (int)T,
+                    (int)D, (float)p, (uint64_t)seed, cur_stream());
+  return out;
+}
+
+void embedding_bwd(const at::Tensor& idx, const at::Tensor& dout,
+                   const c10::optional<at::Tensor>& dwte, const c10::optional<at::Tensor>& dwpe,
+                   double p, int64_t seed) {
+  CHECK_I64(idx); CHECK_BF16(dout); CHECK_CONTIG(dout); CHECK_CONTIG(idx);
+  const int64_t B = idx.size(0), T = idx.size(1), D = dout.size(-1);
+  TORCH_CHECK(dout.numel() == B * T * D, "embedding_bwd: shape mismatch");
+  if (dwte.has_value()) { CHECK_F32(*dwte); TORCH_CHECK(dwte->size(-1) == D); }
+  if (dwpe.has_value()) { CHECK_F32(*dwpe); TORCH_CHECK(dwpe->size(-1) == D && dwpe->size(0) >= T); }
+  DevGuard g(idx.device());
+  mg::embedding_bwd(idx.data_ptr<int64_t>(), bp(dout), fp_opt(dwte), fp_opt(dwpe), (int)(B * T),
+                    (int)T, (int)D, (float)p, (uint64_t)seed, cur_stream());
+}
+
+// ------------------------------------------------------------------------------- cross entropy
+// logits [M, ld] with V valid columns; returns (out[2] = {loss, 1/n_valid}, lse[M])
+std::vector<at::Tensor> xent_fwd(const at::Tensor& logits, const at::Tensor& targets, int64_t V) {
+  CHECK_BF16(logits); CHECK_I64(targets); CHECK_CONTIG(logits); CHECK_CONTIG(targets);
+  const int64_t ld = logits.size(-1), M = logits.numel() / ld;
+  TORCH_CHECK(targets.numel() == M && V <= ld && ld % 8 == 0, "xent: shape mismatch");
+  DevGuard g(logits.device());
+  auto opts = logits.options().dtype(at::kFloat);
+  auto loss_row = at::empty({M}, opts);
+  auto lse = at::empty({M}, opts);
+  auto out = at::empty({2}, opts);
+  mg::xent_fwd(bp(logits), targets.data_ptr<int64_t>(), fp(loss_row), fp(lse), fp(out), (int)M,
+               (int)V, (int)ld, cur_stream());
+  return {out, lse};
+}
+
+at::Tensor xent_bwd(const at::Tensor& logits, const at::Tensor& targets, const at::Tensor& lse,
+                    const at::Tensor& gscale, const at::Tensor& out, int64_t V) {
+  CHECK_BF16(logits); CHECK_I64(targets); CHECK_F32(lse); CHECK_F32(gscale); CHECK_F32(out);
+  const int64_t ld = logits.size(-1), M = logits.numel() / ld;
+  TORCH_CHECK(targets.numel() == M && lse.numel() == M, "xent_bwd: shape mismatch");
+  DevGuard g(logits.device());
+  auto dl = at::empty_like(logits);
+  mg::xent_bwd(bp(logits), targets.data_ptr<int64_t>(), fp(lse), fp(gscale), fp(out) + 1, bp(dl),
+               (int)M, (int)V, (int)ld, cur_stream());
+  return dl;
+}
+
+// ------------------------------------------------------------------------------- optimizer
+void grad_sumsq(const at::Tensor& grad, double grad_scale, const at::Tensor& out) {
+  CHECK_F32(grad); CHECK_F32(out); CHECK_CONTIG(grad);
+  TORCH_CHECK(out.numel() >= 2);
+  DevGuard g(grad.device());
+  auto ws = at::empty({(int64_t)(mg::grad_norm_workspace() / 4)}, grad.options());
+  mg::grad_sumsq(fp(grad), grad.numel(), (float)grad_scale, fp(ws), fp(out), cur_stream());
+}
+
+void adamw_step(const at::Tensor& chunk_start, const at::Tensor& chunk_len,
+                const at::Tensor& chunk_wd, const at::Tensor& master, const at::Tensor& param,
+                const at::Tensor& grad, const at::Tensor& m, const at::Tensor& v,
+                const at::Tensor& norm, double lr, double b1, double b2, double eps, int64_t step,
+                double grad_scale, double clip) {
+  CHECK_I64(chunk_start); CHECK_DEV(chunk_len); CHECK_F32(chunk_wd);
+  TORCH_CHECK(chunk_len.scalar_type() == at::kInt, "chunk_len must be int32");
+  CHECK_F32(master); CHECK_BF16(param); CHECK_F32(grad); CHECK_F32(m); CHECK_F32(v); CHECK_F32(norm);
+  const int64_t n = master.numel();
+  TORCH_CHECK(param.numel() == n && grad.numel() == n && m.numel() == n && v.numel() == n,
+              "adamw: flat buffer size mismatch");
+  TORCH_CHECK(chunk_start.numel() == chunk_len.numel() && chunk_wd.numel() == chunk_len.numel());
+  DevGuard g(master.device());
+  mg::adamw_step(chunk_start.data_ptr<int64_t>(), chunk_len.data_ptr<int>(), fp(chunk_wd),
+                 (int)chunk_len.numel(), fp(master), bp(param), fp(grad), fp(m), fp(v), fp(norm),
+                 (float)lr, (float)b1, (float)b2, (float)eps, (int)step, (float)grad_scale,
+                 (float)clip, cur_stream());
+}
+
+void f32_to_bf16(const at::Tensor& src, const at::Tensor& dst) {
+  CHECK_F32(src); CHECK_BF16(dst);
+  TORCH_CHECK(src.numel() == dst.numel() && src.is_contiguous() && dst.is_contiguous());
+  DevGuard g(src.device());
+  mg::f32_to_bf16(fp(src), bp(dst), src.numel(), cur_stream());
+}
+
+// ------------------------------------------------------------------------------- elementwise
+at::Tensor bias_act(const at::Tensor& x, const c10::optional<at::Tensor>& b,
+                    const c10::optional<at::Tensor>& pre, int64_t act) {
+  CHECK_BF16(x); CHECK_CONTIG(x);
+  const int64_t N = x.size(-1), M = x.numel() / N;
+  TORCH_CHECK(N % 8 == 0, "bias_act: N % 8 != 0");
+  if (b.has_value()) { CHECK_BF16(*b); TORCH_CHECK(b->numel() == N); }
+  if (pre.has_value()) { CHECK_BF16(*pre); TORCH_CHECK(pre->numel() == x.numel()); }
+  DevGuard g(x.device());
+  auto y = at::empty_like(x);
+  mg::bias_act_fwd(bp(x), bp_opt(b), bp_opt(pre), bp(y), M, (int)N, (int)act, cur_stream());
+  return y;
+}
+
+at::Tensor bias_dropout_residual(const at::Tensor& x, const c10::optional<at::Tensor>& b,
+                                 const at::Tensor& r, double p, int64_t seed) {
+  CHECK_BF16(x); CHECK_BF16(r); CHECK_CONTIG(x); CHECK_CONTIG(r);
+  const int64_t N = x.size(-1), M = x.numel() / N;
+  TORCH_CHECK(N % 8 == 0 && r.numel() == x.numel(), "bias_dropout_residual: shape mismatch");
+  if (b.has_value()) { CHECK_BF16(*b); TORCH_CHECK(b->numel() == N); }
+  DevGuard g(x.device());
+  auto y = at::empty_like(x);
+  mg::bias_dropout_residual(bp(x), bp_opt(b), bp(r), bp(y), M, (int)N, (float)p, (uint64_t)seed,
+                            cur_stream());
+  return y;
+}
+
+at::Tensor gelu_bwd(const at::Tensor& dy, const at::Tensor& pre) {
+  CHECK_BF16(dy); CHECK_BF16(pre); CHECK_CONTIG(dy); CHECK_CONTIG(pre);
+  TORCH_CHECK(dy.numel() == pre.numel() && dy.numel() % 8 == 0);
+  DevGuard g(dy.device());
+  auto dx = at::empty_like(dy);
+  mg::gelu_bwd(bp(dy), bp(pre), bp(dx), dy.numel(), cur_stream());
+  return dx;
+}
+
+at::Tensor dropout_bwd(const at::Tensor& dy, double p, int64_t seed) {
+  CHECK_BF16(dy); CHECK_CONTIG(dy);
+  TORCH_CHECK(dy.numel() % 8 == 0);
+  DevGuard g(dy.device());
+  auto dx = at::empty_like(dy);
+  mg::dropout_bwd(bp(dy), bp(dx), dy.numel(), (float)p, (uint64_t)seed, cur_stream());
+  return dx;
+}
+
+void bias_grad(const at::Tensor& dy, const at::Tensor& db) {
+  CHECK_BF16(dy); CHECK_F32(db); CHECK_CONTIG(dy);
+  const int64_t N = dy.size(-1), M = dy.numel() / N;
+  TORCH_CHECK(N % 8 == 0 && db.numel() == N, "bias_grad: shape mismatch");
+  DevGuard g(dy.device());
+  mg::bias_grad(bp(dy), fp(db), M, (int)N, cur_stream());
+}
+
+// ------------------------------------------------------------------------------- gemm
+// layout 0 (NT): c[M, ldc] = a[M, K] @ b[N, K]^T           (+ epilogue)
+// layout 1 (NN): c[M, N]   = a[M, K] @ b[Kb, N]            (b rows >= Kb read as zero)
+// layout 2 (TN): c[M, N]  += a[K, Ma]^T @ b[K, N]   fp32 c (M <= Ma store rows)
+void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t layout, int64_t epi,
+          const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
+          const c10::optional<at::Tensor>& resid, double p, int64_t seed, int64_t M, int64_t N) {
+  CHECK_BF16(a); CHECK_BF16(b); CHECK_DEV(c);
+  CHECK_CONTIG(a); CHECK_CONTIG(b); CHECK_CONTIG(c);
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm: 2-D operands required");
+  TORCH_CHECK(layout >= 0 && layout <= 2 && epi >= 0 && epi <= 4, "gemm: bad layout/epilogue");
+  const int64_t lda = a.size(1), ldb = b.size(1), ldc = c.size(1);
+  TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0, "gemm: row strides must be multiples of 8");
+  TORCH_CHECK(M > 0 && N > 0 && M <= c.size(0) && N <= ldc, "gemm: output bounds");
+  int64_t K, a_ext, b_ext, ka, kb;
+  if (layout == 0) {
+    K = lda; ka = lda; kb = ldb; a_ext = a.size(0); b_ext = b.size(0);
+    TORCH_CHECK(lda == ldb, "gemm NT: K mismatch");
+    TORCH_CHECK(M <= a_ext && N <= (epi == 0 ? ldc : b_ext), "gemm NT: shape mismatch");
+    TORCH_CHECK(c.scalar_type() == at::kBFloat16, "gemm NT: bf16 output");
+  } else if (layout == 1) {
+    K = lda; ka = lda; kb = b.size(0); a_ext = a.size(0); b_ext = ldb;
+    TORCH_CHECK(kb <= K && M <= a_ext && N <= ldb && epi % 4 == 0, "gemm NN: shape mismatch");
+    TORCH_CHECK(c.scalar_type() == at::kBFloat16, "gemm NN: bf16 output");
+  } else {
+    K = a.size(0); ka = K; kb = b.size(0); a_ext = lda; b_ext = ldb;
+    TORCH_CHECK(kb == K && M <= lda && N <= ldb && epi == 0, "gemm TN: shape mismatch");
+    TORCH_CHECK(c.scalar_type() == at::kFloat, "gemm TN: fp32 accumulate output");
+  }
+  TORCH_CHECK(K % 8 == 0, "gemm: K must be a multiple of 8");
+  const bf16_t* bias_p = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    CHECK_BF16(*bias);
+    TORCH_CHECK(bias->numel() >= N, "gemm: bias too short");
+    bias_p = bp(*bias);
+  }
+  bf16_t* aux_p = nullptr;
+  if (epi == 2 || epi == 4) {
+    TORCH_CHECK(aux.has_value() && aux->defined(), "gemm: epilogue needs aux");
+    CHECK_BF16(*aux); CHECK_CONTIG(*aux);
+    TORCH_CHECK(aux->numel() == c.numel(), "gemm: aux shape");
+    aux_p = bp(*aux);
+  }
+  const bf16_t* res_p = nullptr;
+  if (epi == 3) {
+    TORCH_CHECK(resid.has_value() && resid->defined(), "gemm: epilogue needs resid");
+    CHECK_BF16(*resid); CHECK_CONTIG(*resid);
+    TORCH_CHECK(resid->numel() == c.numel() && ldc == N, "gemm: resid shape");
+    res_p = bp(*resid);
+  }
+  DevGuard g(a.device());
+  mg::gemm((int)layout, (int)epi, bp(a), bp(b), c.data_ptr(), lda, ldb, ldc, (int)M, (int)N, (int)K,
+           (int)a_ext, (int)b_ext, (int)ka, (int)kb, bias_p, aux_p, res_p, (float)p, (uint64_t)seed,
+           cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "mingpt_distributed_amd gfx950 kernels";
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_bwd", &embedding_bwd);
+  m.def("xent_fwd", &xent_fwd);
+  m.def("xent_bwd", &xent_bwd);
+  m.def("grad_sumsq", &grad_sumsq);
+  m.def("adamw_step", &adamw_step);
+  m.def("f32_to_bf16", &f32_to_bf16);
+  m.def("bias_act", &bias_act);
+  m.def("bias_dropout_residual", &bias_dropout_residual);
+  m.def("gelu_bwd", &gelu_bwd);
+  m.def("dropout_bwd", &dropout_bwd);
+  m.def("bias_grad", &bias_grad);
+  m.def("gemm", &gemm);
+}

@@ -1,0 +1,145 @@
+// Shared device helpers for the gfx950 (CDNA4, MI355X) kernels.
+//
+// Conventions used by every kernel in csrc/kernels:
+//  * bf16 tensors travel as raw uint16_t bit patterns; they are loaded 8 at a time
+//    (16 B per lane, the coalescing sweet spot on CDNA) and widened to fp32 with a shift.
+//  * a wave is 64 lanes; block sizes are multiples of 64.
+//  * every launch takes an explicit hipStream_t (the caller's current torch stream), so a
+//    whole step can be captured into a hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MG_DEVICE __device__ __forceinline__
+
+namespace mg {
+
+constexpr int kWave = 64;
+
+typedef uint16_t bf16_t;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+MG_DEVICE float bf2f(uint32_t v) { return __uint_as_float(v << 16); }
+
+MG_DEVICE bf16_t f2bf(float f) {
+  __bf16 h = (__bf16)f;  // gfx950: v_cvt_pk_bf16_f32, round-to-nearest-even, NaN-preserving
+  return __builtin_bit_cast(bf16_t, h);
+}
+
+MG_DEVICE uint32_t pack2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// 8 x bf16 <-> 8 x f32 through one 16-byte vector.
+MG_DEVICE void unpack8(const uint4& u, float (&f)[8]) {
+  f[0] = bf2f(u.x & 0xffffu); f[1] = bf2f(u.x >> 16);
+  f[2] = bf2f(u.y & 0xffffu); f[3] = bf2f(u.y >> 16);
+  f[4] = bf2f(u.z & 0xffffu); f[5] = bf2f(u.z >> 16);
+  f[6] = bf2f(u.w & 0xffffu); f[7] = bf2f(u.w >> 16);
+}
+
+MG_DEVICE uint4 pack8(const float (&f)[8]) {
+  return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+}
+
+MG_DEVICE uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
+MG_DEVICE void st16(void* p, const uint4& v) { *reinterpret_cast<uint4*>(p) = v; }
+
+// ---------------------------------------------------------------- wave / block reductions
+MG_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+MG_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Sum over a block of NW waves; `red` must hold NW floats of LDS. Result broadcast to all.
+template <int NW>
+MG_DEVICE float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) t += red[i];
+  return t;
+}
+
+template <int NW>
+MG_DEVICE float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) t = fmaxf(t, red[i]);
+  return t;
+}
+
+// ---------------------------------------------------------------- Philox-4x32-10 RNG
+// Counter-based: the dropout mask of element e under seed s is a pure function of (s, e), so
+// the backward pass regenerates it instead of storing it.
+MG_DEVICE uint4 philox4x32(uint4 ctr, uint2 key) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = ctr.x * 0xD2511F53u, hi0 = __umulhi(ctr.x, 0xD2511F53u);
+    const uint32_t lo1 = ctr.z * 0xCD9E8D57u, hi1 = __umulhi(ctr.z, 0xCD9E8D57u);
+    ctr = make_uint4(hi1 ^ ctr.y ^ key.x, lo1, hi0 ^ ctr.w ^ key.y, lo0);
+    key.x += 0x9E3779B9u;
+    key.y += 0xBB67AE85u;
+  }
+  return ctr;
+}
+
+// 4 random words for the aligned group of 4 elements starting at e4*4.
+MG_DEVICE uint4 rand4(uint64_t seed, uint64_t e4) {
+  return philox4x32(make_uint4((uint32_t)e4, (uint32_t)(e4 >> 32), 0x5eed5eedu, 0u),
+                    make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+}
+
+// keep-threshold: keep element iff rand >= thr, thr = p * 2^32.
+inline uint32_t dropout_threshold(float p) {
+  double t = (double)p * 4294967296.0;
+  if (t >= 4294967295.0) return 0xffffffffu;
+  return (uint32_t)t;
+}
+
+// Apply dropout to 8 consecutive elements starting at e (e % 8 == 0).
+MG_DEVICE void dropout8(float (&v)[8], uint64_t seed, uint64_t e, uint32_t thr, float scale) {
+  const uint4 r0 = rand4(seed, e >> 2), r1 = rand4(seed, (e >> 2) + 1);
+  const uint32_t r[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (r[i] >= thr) ? v[i] * scale : 0.f;
+}
+
+// ---------------------------------------------------------------- GELU (tanh approximation)
+constexpr float kGeluK0 = 0.7978845608028654f;  // sqrt(2/pi)
+constexpr float kGeluK1 = 0.044715f;
+
+MG_DEVICE float gelu_f(float x) {
+  const float u = kGeluK0 * (x + kGeluK1 * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+
+MG_DEVICE float gelu_grad(float x) {
+  const float x2 = x * x;
+  const float u = kGeluK0 * (x + kGeluK1 * x2 * x);
+  const float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kGeluK0 * (1.f + 3.f * kGeluK1 * x2);
+}
+
+inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace mg

@@ -1,0 +1,57 @@
+// Host-side launch API of every gfx950 kernel in csrc/kernels.  Pure HIP: no torch headers,
+// raw device pointers + an explicit stream, so the kernels can be driven by the torch binding
+// (csrc/bindings.cpp), by native tools, or captured into a hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace mg {
+typedef uint16_t bf16_t;
+
+// layernorm.hip
+void layernorm_fwd(const bf16_t* x, const bf16_t* w, const bf16_t* b, bf16_t* y, float* mean,
+                   float* rstd, int M, int D, float eps, hipStream_t stream);
+void layernorm_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const float* mean,
+                   const float* rstd, bf16_t* dx, float* dw, float* db, float* workspace, int M,
+                   int D, hipStream_t stream);
+size_t layernorm_bwd_workspace(int M, int D);
+
+// embedding.hip
+void embedding_fwd(const int64_t* idx, const bf16_t* wte, const bf16_t* wpe, bf16_t* out, int M,
+                   int T, int D, float p, uint64_t seed, hipStream_t stream);
+void embedding_bwd(const int64_t* idx, const bf16_t* dout, float* dwte, float* dwpe, int M, int T,
+                   int D, float p, uint64_t seed, hipStream_t stream);
+
+// xent.hip
+void xent_fwd(const bf16_t* logits, const int64_t* targets, float* loss_row, float* lse, float* out,
+              int M, int V, int ld, hipStream_t stream);
+void xent_bwd(const bf16_t* logits, const int64_t* targets, const float* lse, const float* gscale,
+              const float* inv_n, bf16_t* dlogits, int M, int V, int ld, hipStream_t stream);
+
+// adamw.hip
+size_t grad_norm_workspace();
+void grad_sumsq(const float* grad, long n, float grad_scale, float* workspace, float* out,
+                hipStream_t stream);
+void adamw_step(const int64_t* chunk_start, const int* chunk_len, const float* chunk_wd, int n_chunks,
+                float* master, bf16_t* param, const float* grad, float* m, float* v,
+                const float* norm, float lr, float b1, float b2, float eps, int step,
+                float grad_scale, float clip, hipStream_t stream);
+void f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t stream);
+
+// elementwise.hip
+void bias_act_fwd(const bf16_t* x, const bf16_t* b, bf16_t* pre, bf16_t* y, long M, int N, int act,
+                  hipStream_t stream);
+void bias_dropout_residual(const bf16_t* x, const bf16_t* b, const bf16_t* r, bf16_t* y, long M,
+                           int N, float p, uint64_t seed, hipStream_t stream);
+void gelu_bwd(const bf16_t* dy, const bf16_t* pre, bf16_t* dx, long n, hipStream_t stream);
+void dropout_bwd(const bf16_t* dy, bf16_t* dx, long n, float p, uint64_t seed, hipStream_t stream);
+void bias_grad(const bf16_t* dy, float* db, long M, int N, hipStream_t stream);
+
+// gemm.hip -- layout 0 NT (fwd), 1 NN (dgrad), 2 TN (wgrad, fp32 accumulate)
+// epi: 0 none, 1 bias, 2 bias+gelu (pre -> aux), 3 resid + dropout(acc + bias), 4 acc*gelu'(aux)
+void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long lda, long ldb,
+          long ldc, int M, int N, int K, int a_ext, int b_ext, int ka, int kb, const bf16_t* bias,
+          bf16_t* aux, const bf16_t* resid, float p, uint64_t seed, hipStream_t stream);
+
+}  // namespace mg

@@ -1,0 +1,139 @@
+// Fused AdamW + global-norm gradient clipping over flat buffers (gfx950).
+//
+// Replaces torch.optim.AdamW (/root/reference/mingpt/model.py:117-121) and
+// clip_grad_norm (/root/reference/mingpt/trainer.py:129-130).  The framework keeps every
+// parameter as a view into ONE flat buffer per dtype (bf16 compute params, fp32 master
+// weights, fp32 grads, fp32 exp_avg / exp_avg_sq), so a whole optimizer step is 3 launches:
+//   1. grad_sumsq_partial: per-block sum of squares of the (scaled) grads,
+//   2. grad_sumsq_final:   one block folds the partials -> {sumsq, norm} on the device,
+//   3. adamw_kernel:       multi-tensor-apply style: block b owns chunk b of a host-built chunk
+//                          table (chunks never straddle parameters, so weight decay is a
+//                          per-chunk constant).  The clip coefficient is computed on device from
+//                          step 2's output: no host sync, graph-capturable.
+// Numerics match torch.optim.AdamW (decoupled decay p *= 1 - lr*wd, bias corrections, eps
+// added after dividing sqrt(v) by sqrt(bc2)).
+#include "common.h"
+#include "kernels.h"
+
+using namespace mg;
+
+namespace {
+
+__global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restrict__ g, long n,
+                                                            float* __restrict__ part) {
+  __shared__ float red[4];
+  float s = 0.f;
+  const long n4 = n >> 2;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const float4 v = g4[i];
+    s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  for (long i = (n4 << 2) + (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    s += g[i] * g[i];
+  s = block_sum<4>(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void sumsq_final_kernel(const float* __restrict__ part, int G,
+                                                          float grad_scale, float* __restrict__ out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < G; i += 256) s += part[i];
+  s = block_sum<4>(s, red);
+  if (threadIdx.x == 0) {
+    out[0] = s;
+    out[1] = sqrtf(s) * grad_scale;
+  }
+}
+
+__global__ __launch_bounds__(256) void adamw_kernel(
+    const int64_t* __restrict__ chunk_start, const int* __restrict__ chunk_len,
+    const float* __restrict__ chunk_wd, float* __restrict__ master, bf16_t* __restrict__ param,
+    const float* __restrict__ grad, float* __restrict__ m, float* __restrict__ v,
+    const float* __restrict__ norm, float lr, float b1, float b2, float eps, float bc1,
+    float bc2_sqrt, float grad_scale, float clip) {
+  const long s0 = chunk_start[blockIdx.x];
+  const int len = chunk_len[blockIdx.x];
+  const float wd = chunk_wd[blockIdx.x];
+  float gs = grad_scale;
+  if (clip > 0.f) {
+    const float tn = sqrtf(norm[0]) * grad_scale;
+    const float coef = clip / (tn + 1e-6f);
+    if (coef < 1.f) gs *= coef;
+  }
+  const float decay = 1.f - lr * wd;
+  const float step = lr / bc1;
+  for (int i = threadIdx.x * 4; i < len; i += 256 * 4) {
+    const long e = s0 + i;
+    if (i + 4 <= len) {
+      float4 p = *reinterpret_cast<float4*>(master + e);
+      const float4 g = *reinterpret_cast<const float4*>(grad + e);
+      float4 mm = *reinterpret_cast<float4*>(m + e);
+      float4 vv = *reinterpret_cast<float4*>(v + e);
+      float pa[4] = {p.x, p.y, p.z, p.w}, ga[4] = {g.x, g.y, g.z, g.w};
+      float ma[4] = {mm.x, mm.y, mm.z, mm.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float gg = ga[j] * gs;
+        ma[j] = b1 * ma[j] + (1.f - b1) * gg;
+        va[j] = b2 * va[j] + (1.f - b2) * gg * gg;
+        pa[j] = pa[j] * decay - step * ma[j] / (sqrtf(va[j]) / bc2_sqrt + eps);
+      }
+      *reinterpret_cast<float4*>(master + e) = make_float4(pa[0], pa[1], pa[2], pa[3]);
+      *reinterpret_cast<float4*>(m + e) = make_float4(ma[0], ma[1], ma[2], ma[3]);
+      *reinterpret_cast<float4*>(v + e) = make_float4(va[0], va[1], va[2], va[3]);
+      *reinterpret_cast<uint2*>(param + e) = make_uint2(pack2(pa[0], pa[1]), pack2(pa[2], pa[3]));
+    } else {
+      for (int j = 0; j < 4 && i + j < len; ++j) {
+        const long k = e + j;
+        const float gg = grad[k] * gs;
+        const float mj = b1 * m[k] + (1.f - b1) * gg;
+        const float vj = b2 * v[k] + (1.f - b2) * gg * gg;
+        const float pj = master[k] * decay - step * mj / (sqrtf(vj) / bc2_sqrt + eps);
+        m[k] = mj;
+        v[k] = vj;
+        master[k] = pj;
+        param[k] = f2bf(pj);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restrict__ src,
+                                                          bf16_t* __restrict__ dst, long n) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    dst[i] = f2bf(src[i]);
+}
+
+}  // namespace
+
+namespace mg {
+
+constexpr int kNormBlocks = 1024;
+
+size_t grad_norm_workspace() { return sizeof(float) * kNormBlocks; }
+
+void grad_sumsq(const float* grad, long n, float grad_scale, float* workspace, float* out,
+                hipStream_t stream) {
+  sumsq_partial_kernel<<<kNormBlocks, 256, 0, stream>>>(grad, n, workspace);
+  sumsq_final_kernel<<<1, 256, 0, stream>>>(workspace, kNormBlocks, grad_scale, out);
+}
+
+void adamw_step(const int64_t* chunk_start, const int* chunk_len, const float* chunk_wd, int n_chunks,
+                float* master, bf16_t* param, const float* grad, float* m, float* v,
+                const float* norm, float lr, float b1, float b2, float eps, int step,
+                float grad_scale, float clip, hipStream_t stream) {
+  const float bc1 = 1.f - powf(b1, (float)step);
+  const float bc2_sqrt = sqrtf(1.f - powf(b2, (float)step));
+  adamw_kernel<<<n_chunks, 256, 0, stream>>>(chunk_start, chunk_len, chunk_wd, master, param, grad,
+                                             m, v, norm, lr, b1, b2, eps, bc1, bc2_sqrt, grad_scale,
+                                             clip);
+}
+
+void f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t stream) {
+  const int grid = (int)std::min<long>(4096, (n + 255) / 256);
+  f32_to_bf16_kernel<<<grid, 256, 0, stream>>>(src, dst, n);
+}
+
+}  // namespace mg

@@ -1,0 +1,203 @@
+// LayerNorm forward / backward for gfx950.
+//
+// Replaces the reference's three ATen LayerNorms per block (ln_1, ln_2, ln_ff:
+// /root/reference/mingpt/model.py:176,178,248).  Layout: x is [M, D] bf16 row-major.
+//
+// Forward: one wave per row, 4 rows per 256-thread block; each lane holds NV chunks of 8
+// contiguous bf16 (16-B loads), so the row is read from HBM exactly once and the two-pass
+// (mean, then centred variance) statistics come from registers.  mean/rstd are saved in fp32.
+//
+// Backward: same row mapping.  dx is produced per row; dgamma/dbeta are accumulated per wave in
+// registers over a grid-stride loop, reduced across the block's waves through LDS into a
+// [grid, D] fp32 partial slab, and a second kernel sums the slab deterministically and adds it
+// into the fp32 main-grad buffers (no float atomics, bitwise reproducible).
+#include "common.h"
+#include "kernels.h"
+
+using namespace mg;
+
+namespace {
+
+template <int NV>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ x,
+                                                     const bf16_t* __restrict__ w,
+                                                     const bf16_t* __restrict__ b,
+                                                     bf16_t* __restrict__ y, float* __restrict__ mean,
+                                                     float* __restrict__ rstd, int M, int D,
+                                                     float eps) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const bf16_t* xr = x + row * D;
+  float v[NV][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 8;
+    if (c < D) {
+      unpack8(ld16(xr + c), v[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[i][j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
+  }
+  const float mu = wave_sum(s) / D;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 8;
+    if (c < D) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[i][j] - mu;
+        ss += d * d;
+      }
+    }
+  }
+  const float rs = rsqrtf(wave_sum(ss) / D + eps);
+  if (lane == 0) {
+    mean[row] = mu;
+    rstd[row] = rs;
+  }
+  bf16_t* yr = y + row * D;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 8;
+    if (c < D) {
+      float wf[8], bf[8], o[8];
+      unpack8(ld16(w + c), wf);
+      unpack8(ld16(b + c), bf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mu) * rs * wf[j] + bf[j];
+      st16(yr + c, pack8(o));
+    }
+  }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                     const bf16_t* __restrict__ x,
+                                                     const bf16_t* __restrict__ w,
+                                                     const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd,
+                                                     bf16_t* __restrict__ dx,
+                                                     float* __restrict__ part, int M, int D) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float gacc[NV][8], bacc[NV][8], wf[NV][8];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 8;
+    if (c < D) unpack8(ld16(w + c), wf[i]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      gacc[i][j] = 0.f;
+      bacc[i][j] = 0.f;
+      if (c >= D) wf[i][j] = 0.f;
+    }
+  }
+  for (long row = (long)blockIdx.x * 4 + wid; row < M; row += (long)gridDim.x * 4) {
+    const float mu = mean[row], rs = rstd[row];
+    const bf16_t* xr = x + row * D;
+    const bf16_t* dyr = dy + row * D;
+    float xh[NV][8], g[NV][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      if (c < D) {
+        float xv[8];
+        unpack8(ld16(xr + c), xv);
+        unpack8(ld16(dyr + c), g[i]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[i][j] = (xv[j] - mu) * rs;
+          const float gw = g[i][j] * wf[i][j];
+          s1 += gw;
+          s2 += gw * xh[i][j];
+          gacc[i][j] += g[i][j] * xh[i][j];
+          bacc[i][j] += g[i][j];
+        }
+      }
+    }
+    s1 = wave_sum(s1) / D;
+    s2 = wave_sum(s2) / D;
+    bf16_t* dxr = dx + row * D;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      if (c < D) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rs * (g[i][j] * wf[i][j] - s1 - xh[i][j] * s2);
+        st16(dxr + c, pack8(o));
+      }
+    }
+  }
+  // reduce the 4 waves' column partials through LDS, then write this block's partial row.
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [4][2*D]
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 8;
+    if (c < D) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[wid * 2 * D + c + j] = gacc[i][j];
+        red[wid * 2 * D + D + c + j] = bacc[i][j];
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * D; c += 256) {
+    part[(long)blockIdx.x * 2 * D + c] = red[c] + red[2 * D + c] + red[4 * D + c] + red[6 * D + c];
+  }
+}
+
+// Sum partial slab [G, 2D] over G; add into dw (first D) and db (second D) main grads.
+__global__ __launch_bounds__(256) void ln_bwd_reduce_kernel(const float* __restrict__ part,
+                                                            float* __restrict__ dw,
+                                                            float* __restrict__ db, int G, int D) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= 2 * D) return;
+  float s = 0.f;
+  for (int g = 0; g < G; ++g) s += part[(long)g * 2 * D + c];
+  if (c < D)
+    dw[c] += s;
+  else
+    db[c - D] += s;
+}
+
+}  // namespace
+
+namespace mg {
+
+int ln_bwd_grid(int M) { return M / 4 < 512 ? (M + 3) / 4 : 512; }
+
+#define MG_LN_DISPATCH(KERNEL, ...)                                                   \
+  do {                                                                                \
+    if (D <= 512) KERNEL<1><<<grid, 256, smem, stream>>>(__VA_ARGS__);                \
+    else if (D <= 1024) KERNEL<2><<<grid, 256, smem, stream>>>(__VA_ARGS__);          \
+    else if (D <= 2048) KERNEL<4><<<grid, 256, smem, stream>>>(__VA_ARGS__);          \
+    else KERNEL<8><<<grid, 256, smem, stream>>>(__VA_ARGS__);                         \
+  } while (0)
+
+void layernorm_fwd(const bf16_t* x, const bf16_t* w, const bf16_t* b, bf16_t* y, float* mean,
+                   float* rstd, int M, int D, float eps, hipStream_t stream) {
+  const int grid = cdiv(M, 4);
+  const size_t smem = 0;
+  MG_LN_DISPATCH(ln_fwd_kernel, x, w, b, y, mean, rstd, M, D, eps);
+}
+
+void layernorm_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const float* mean,
+                   const float* rstd, bf16_t* dx, float* dw, float* db, float* workspace, int M,
+                   int D, hipStream_t stream) {
+  const int grid = ln_bwd_grid(M);
+  const size_t smem = sizeof(float) * 8 * D;
+  MG_LN_DISPATCH(ln_bwd_kernel, dy, x, w, mean, rstd, dx, workspace, M, D);
+  ln_bwd_reduce_kernel<<<cdiv(2 * D, 256), 256, 0, stream>>>(workspace, dw, db, grid, D);
+}
+
+size_t layernorm_bwd_workspace(int M, int D) { return sizeof(float) * (size_t)ln_bwd_grid(M) * 2 * D; }
+
+}  // namespace mg

@@ -1,0 +1,70 @@
+"""GEMM front-end for the GPU path: the three layouts a transformer step needs, each with the
+epilogue fused where the data is produced.
+
+* ``gemm_nt``      C[M,N] = A[M,K] @ B[N,K]^T   (forward; B is an nn.Linear weight [out, in])
+                   epilogues: ``none`` | ``bias`` | ``gelu`` (bias + tanh-GELU, also stores the
+                   pre-activation) | ``resid`` (R + dropout(acc + bias))
+* ``gemm_nn``      C[M,N] = A[M,K] @ B[K,N]     (data gradient dX = dY @ W)
+                   epilogue: ``none`` | ``gelu_bwd`` (multiply by GELU'(pre))
+* ``gemm_tn_acc``  C[N,K] += A[M,N]^T @ B[M,K] (weight gradient, fp32 accumulate into main_grad)
+
+All three run on the hand-written MFMA kernel in ``csrc/kernels/gemm.hip`` (``_C.gemm``).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ._ext import ext
+
+EPI_NONE, EPI_BIAS, EPI_GELU, EPI_RESID, EPI_GELU_BWD = 0, 1, 2, 3, 4
+
+
+def _check2d(t, name):
+    if t.dim() != 2 or not t.is_contiguous():
+        raise ValueError(f"{name} must be a contiguous 2-D tensor, got {tuple(t.shape)}")
+
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: Optional[torch.Tensor] = None,
+            epi: str = "none", resid: Optional[torch.Tensor] = None, p: float = 0.0, seed: int = 0,
+            pre_out: Optional[torch.Tensor] = None, ld: Optional[int] = None) -> torch.Tensor:
+    """C = A @ B^T with a fused epilogue. ``ld`` pads the output row stride (logits)."""
+    _check2d(a, "A")
+    _check2d(b, "B")
+    M, K = a.shape
+    N = b.shape[0]
+    ld = ld or N
+    c = torch.empty((M, ld), dtype=torch.bfloat16, device=a.device)
+    code = {"none": EPI_NONE, "bias": EPI_BIAS, "gelu": EPI_GELU, "resid": EPI_RESID}[epi]
+    if code == EPI_BIAS and bias is None:
+        code = EPI_NONE
+    ext().gemm(a, b, c, 0, code, bias, pre_out, resid, float(p), int(seed), M, N)
+    return c
+
+
+def gemm_nn(a: torch.Tensor, b: torch.Tensor, *, epi: str = "none",
+            aux: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """C = A @ B (B row-major [K, N]); ``gelu_bwd`` multiplies by GELU'(aux)."""
+    _check2d(a, "A")
+    _check2d(b, "B")
+    M, K = a.shape
+    N = b.shape[1]
+    c = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    code = {"none": EPI_NONE, "gelu_bwd": EPI_GELU_BWD}[epi]
+    ext().gemm(a, b, c, 1, code, None, aux, None, 0.0, 0, M, N)
+    return c
+
+
+def gemm_tn_acc(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, n_valid: Optional[int] = None):
+    """c[N, K] += A[M, N]^T @ B[M, K]  (fp32 c). ``n_valid`` limits the rows of c written."""
+    _check2d(a, "A")
+    _check2d(b, "B")
+    M, N = a.shape
+    K = b.shape[1]
+    if n_valid is not None:
+        N = n_valid
+    if c.dtype != torch.float32 or c.shape[0] < N or c.shape[1] != K:
+        raise ValueError("gemm_tn_acc: c must be fp32 [N, K]")
+    ext().gemm(a, b, c, 2, EPI_NONE, None, None, None, 0.0, 0, N, K)
+    return c

@@ -1,0 +1,90 @@
+"""MFMA GEMM (csrc/kernels/gemm.hip) vs fp32 PyTorch, all layouts and epilogues, tail shapes."""
+import pytest
+import torch
+
+from mingpt_distributed_amd.ops import gemm as G
+from mingpt_distributed_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _bf(*shape, seed=0, scale=1.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(DEV, torch.bfloat16)
+
+
+def _check(out, ref, K):
+    tol = 2e-2 * (K ** 0.5) * 0.25 + 2e-2
+    torch.testing.assert_close(out.float(), ref, atol=tol, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 768), (200, 72, 136), (1000, 2304, 768),
+                                   (64, 16, 48)])
+def test_nt_plain_bias(M, N, K):
+    a, b, bias = _bf(M, K, seed=1), _bf(N, K, seed=2), _bf(N, seed=3)
+    ref = a.float() @ b.float().t()
+    _check(G.gemm_nt(a, b), ref, K)
+    _check(G.gemm_nt(a, b, bias=bias, epi="bias"), ref + bias.float(), K)
+
+
+def test_nt_identity_asymmetric():
+    # A = I catches a transposed C write (guide §3: always A=I with asymmetric B)
+    K = 128
+    a = torch.eye(K, device=DEV, dtype=torch.bfloat16)
+    b = torch.arange(K * K, device=DEV, dtype=torch.float32).reshape(K, K).remainder(97).to(torch.bfloat16)
+    torch.testing.assert_close(G.gemm_nt(a, b).float(), b.float().t())
+
+
+def test_nt_padded_ld_vocab():
+    M, V, K, ld = 130, 1001, 64, 1008
+    a, b = _bf(M, K, seed=4), _bf(V, K, seed=5)
+    out = G.gemm_nt(a, b, ld=ld)
+    assert out.shape == (M, ld)
+    _check(out[:, :V], a.float() @ b.float().t(), K)
+
+
+def test_nt_gelu_and_resid():
+    M, N, K = 300, 256, 192
+    a, b, bias, r = _bf(M, K, seed=6), _bf(N, K, seed=7), _bf(N, seed=8), _bf(M, N, seed=9)
+    pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    out = G.gemm_nt(a, b, bias=bias, epi="gelu", pre_out=pre)
+    z = a.float() @ b.float().t() + bias.float()
+    _check(pre, z, K)
+    _check(out, R.gelu_tanh(z), K)
+    out = G.gemm_nt(a, b, bias=bias, epi="resid", resid=r, p=0.0)
+    _check(out, z + r.float(), K)
+    # dropout mask must match the standalone dropout kernel (same Philox element mapping)
+    out = G.gemm_nt(a, b, bias=bias, epi="resid", resid=r, p=0.3, seed=11)
+    from mingpt_distributed_amd.ops._ext import ext
+    ref = ext().bias_dropout_residual(G.gemm_nt(a, b), bias, r, 0.3, 11)
+    _check(out, ref.float(), K)
+
+
+@pytest.mark.parametrize("M,N,K,Kb", [(256, 768, 2304, 2304), (100, 64, 72, 72), (130, 256, 1008, 1001)])
+def test_nn(M, N, K, Kb):
+    a, b = _bf(M, K, seed=10), _bf(Kb, N, seed=11)
+    if Kb < K:  # padded reduction (lm-head dgrad): A's extra columns are zero
+        a[:, Kb:] = 0
+    ref = a.float()[:, :Kb] @ b.float()
+    _check(G.gemm_nn(a, b), ref, K)
+    pre = _bf(M, N, seed=12)
+    _check(G.gemm_nn(a, b, epi="gelu_bwd", aux=pre),
+           ref * torch.func.grad(lambda x: R.gelu_tanh(x).sum())(pre.float()), K)
+
+
+@pytest.mark.parametrize("Mr,N,K", [(256, 768, 768), (192, 72, 136), (1024, 2304, 64)])
+def test_tn_acc(Mr, N, K):
+    a, b = _bf(Mr, N, seed=13), _bf(Mr, K, seed=14)
+    c = torch.randn(N, K, device=DEV)
+    ref = c + a.float().t() @ b.float()
+    G.gemm_tn_acc(a, b, c)
+    _check(c, ref, Mr)
+
+
+def test_tn_acc_nvalid():
+    Mr, V, ld, K = 128, 1001, 1008, 64
+    a, b = _bf(Mr, ld, seed=15), _bf(Mr, K, seed=16)
+    c = torch.zeros(V, K, device=DEV)
+    G.gemm_tn_acc(a, b, c, n_valid=V)
+    _check(c, a.float()[:, :V].t() @ b.float(), Mr)

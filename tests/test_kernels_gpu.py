@@ -1,0 +1,153 @@
+"""Numerics of the standalone gfx950 kernels vs plain-PyTorch fp32 references.
+
+Each kernel is called through the raw extension (``_C``) so a failure points at one kernel.
+"""
+import math
+
+import pytest
+import torch
+
+from mingpt_distributed_amd.ops import reference as R
+from mingpt_distributed_amd.ops._ext import ext
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _bf(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(DEV, torch.bfloat16)
+
+
+def _close(a, b, atol, rtol=0.02):
+    torch.testing.assert_close(a.float(), b.float(), atol=atol, rtol=rtol)
+
+
+@pytest.mark.parametrize("M,D", [(64, 48), (1000, 768), (257, 1600), (33, 192)])
+def test_layernorm_fwd_bwd(M, D):
+    C = ext()
+    x, w, b = _bf(M, D, seed=1), _bf(D, seed=2) * 0.1 + 1, _bf(D, seed=3) * 0.1
+    y, mean, rstd = C.layernorm_fwd(x, w, b, 1e-5)
+    xr, wr, br = (t.float().requires_grad_() for t in (x, w, b))
+    yr = torch.nn.functional.layer_norm(xr, (D,), wr, br, 1e-5)
+    _close(y, yr, atol=3e-2)
+    torch.testing.assert_close(mean, xr.mean(-1).detach(), atol=1e-3, rtol=1e-3)
+    dy = _bf(M, D, seed=4)
+    yr.backward(dy.float())
+    dw = torch.zeros(D, device=DEV)
+    db = torch.ones(D, device=DEV)  # accumulates into existing main grad
+    dx = C.layernorm_bwd(dy, x, w, mean, rstd, dw, db)
+    _close(dx, xr.grad, atol=5e-2)
+    torch.testing.assert_close(dw, wr.grad, atol=5e-2 * math.sqrt(M) / 4, rtol=2e-2)
+    torch.testing.assert_close(db - 1, br.grad, atol=5e-2 * math.sqrt(M) / 4, rtol=2e-2)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_embedding(p):
+    C = ext()
+    B, T, V, D = 4, 64, 97, 192
+    idx = torch.randint(0, V, (B, T), device=DEV)
+    wte, wpe = _bf(V, D, seed=5), _bf(T * 2, D, seed=6)
+    out = C.embedding_fwd(idx, wte, wpe, p, 1234)
+    ref = wte.float()[idx] + wpe.float()[:T].unsqueeze(0)
+    if p == 0.0:
+        _close(out, ref, atol=2e-2)
+    else:
+        keep = out.float() != 0
+        frac = keep.float().mean().item()
+        assert abs(frac - (1 - p)) < 0.02
+        _close(out.float()[keep], (ref / (1 - p))[keep], atol=3e-2)
+    dout = _bf(B, T, D, seed=7)
+    dwte = torch.zeros(V, D, device=DEV)
+    dwpe = torch.zeros(T * 2, D, device=DEV)
+    C.embedding_bwd(idx, dout, dwte, dwpe, p, 1234)
+    g = dout.float()
+    if p > 0:  # the mask from a forward over an all-ones table (a real output can be exactly 0)
+        ones = C.embedding_fwd(idx, torch.ones_like(wte), torch.zeros_like(wpe), p, 1234)
+        g = g * (ones.float() != 0).float() / (1 - p)
+    ref_wte = torch.zeros(V, D, device=DEV).index_add_(0, idx.flatten(), g.reshape(-1, D))
+    ref_wpe = torch.zeros(T * 2, D, device=DEV)
+    ref_wpe[:T] = g.sum(0)
+    torch.testing.assert_close(dwte, ref_wte, atol=1e-3, rtol=1e-3)
+    torch.testing.assert_close(dwpe, ref_wpe, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("M,V,ld", [(64, 65, 72), (300, 50257, 50304), (17, 3, 8)])
+def test_cross_entropy(M, V, ld):
+    C = ext()
+    logits = _bf(M, ld, scale=3.0, seed=8)
+    tgt = torch.randint(0, V, (M,), device=DEV)
+    tgt[::5] = -1
+    out, lse = C.xent_fwd(logits, tgt, V)
+    lr = logits.float()[:, :V].clone().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(lr, tgt, ignore_index=-1)
+    torch.testing.assert_close(out[0], ref.detach(), atol=1e-3, rtol=1e-3)
+    ref.backward(torch.tensor(2.0, device=DEV))
+    g = torch.tensor([2.0], device=DEV)
+    dl = C.xent_bwd(logits, tgt, lse, g, out, V)
+    _close(dl[:, :V], lr.grad, atol=2e-3)
+    assert (dl[:, V:] == 0).all()
+
+
+def test_adamw_matches_torch():
+    C = ext()
+    sizes = [1000, 37, 4096, 5]
+    wds = [0.1, 0.0, 0.1, 0.0]
+    n = sum(sizes)
+    torch.manual_seed(0)
+    master = torch.randn(n, device=DEV)
+    grad = torch.randn(n, device=DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    param = master.to(torch.bfloat16)
+    # chunk table, chunk <= 1024 elements, never straddling a param
+    starts, lens, cwd = [], [], []
+    off = 0
+    for s, wd in zip(sizes, wds):
+        for c in range(0, s, 1024):
+            starts.append(off + c)
+            lens.append(min(1024, s - c))
+            cwd.append(wd)
+        off += s
+    cs = torch.tensor(starts, device=DEV, dtype=torch.int64)
+    cl = torch.tensor(lens, device=DEV, dtype=torch.int32)
+    cw = torch.tensor(cwd, device=DEV, dtype=torch.float32)
+    ref_params = [torch.nn.Parameter(t.clone()) for t in master.split(sizes)]
+    opt = torch.optim.AdamW([{"params": [p], "weight_decay": wd} for p, wd in zip(ref_params, wds)],
+                            lr=1e-3, betas=(0.9, 0.95))
+    norm = torch.zeros(2, device=DEV)
+    for step in range(1, 4):
+        g = grad * step
+        for p, gg in zip(ref_params, g.split(sizes)):
+            p.grad = gg.clone()
+        total = torch.nn.utils.clip_grad_norm_(ref_params, 1.0)
+        opt.step()
+        C.grad_sumsq(g, 1.0, norm)
+        torch.testing.assert_close(norm[1], total, rtol=1e-4, atol=1e-4)
+        C.adamw_step(cs, cl, cw, master, param, g, m, v, norm, 1e-3, 0.9, 0.95, 1e-8, step, 1.0, 1.0)
+    torch.testing.assert_close(master, torch.cat([p.detach() for p in ref_params]), atol=1e-5, rtol=1e-4)
+    _close(param, master, atol=1e-2)
+
+
+def test_elementwise():
+    C = ext()
+    M, N = 130, 768
+    x, b, r = _bf(M, N, seed=9), _bf(N, seed=10), _bf(M, N, seed=11)
+    pre = torch.empty_like(x)
+    y = C.bias_act(x, b, pre, 1)
+    _close(pre, x.float() + b.float(), atol=2e-2)
+    _close(y, R.gelu_tanh(x.float() + b.float()), atol=2e-2)
+    dy = _bf(M, N, seed=12)
+    xr = (x.float() + b.float()).requires_grad_()
+    R.gelu_tanh(xr).backward(dy.float())
+    _close(C.gelu_bwd(dy, pre), xr.grad, atol=3e-2)
+    out = C.bias_dropout_residual(x, b, r, 0.0, 7)
+    _close(out, r.float() + x.float() + b.float(), atol=3e-2)
+    out = C.bias_dropout_residual(x, b, r, 0.5, 7)
+    kept = (out.float() - r.float()).abs() > 1e-6
+    assert abs(kept.float().mean().item() - 0.5) < 0.03
+    dx = C.dropout_bwd(dy, 0.5, 7)
+    assert ((dx.float() != 0) == kept).float().mean().item() > 0.99
+    db = torch.zeros(N, device=DEV)
+    C.bias_grad(dy, db)
+    torch.testing.assert_close(db, dy.float().sum(0), atol=2e-2, rtol=1e-3)
