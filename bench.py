@@ -1,0 +1,118 @@
+#!/usr/bin/env python
+"""Flagship benchmark: GPT-2 124M, seq 1024, bf16 training throughput (tokens/s, whole node).
+
+Metric/config are the ones BASELINE.json names.  One process per GPU (torchrun env), data
+parallel over RCCL.  Synthetic random-token batches of the exact training shape and random-init
+weights (no datasets or checkpoints are reachable); every timed step is a full training step:
+forward, backward, bucketed all-reduce, global grad-norm clip and fused AdamW update, with the
+reference's dropout (0.1) active.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--model gpt2]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+W untimed warmup steps, then K steps bracketed by barrier + device sync; the max over ranks is
+reported.  ``vs_baseline`` divides by N x the measured single-GPU torch-eager self-baseline of the
+same step, i.e. it is the per-GPU speedup over stock PyTorch-ROCm.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import torch
+
+# single-GPU torch-eager self-baseline, same model/shape/dropout (bench/baseline_torch.py, SDPA
+# attention, B=16 x 1024, MI355X): BASELINE.md "Self-baseline" table.
+BASELINE_TOK_S_PER_GPU = 367595.5
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=16, help="sequences per GPU per step")
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--model", default="gpt2")
+    ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--profile", default="", help="write a torch.profiler trace to this dir")
+    a = ap.parse_args()
+
+    from mingpt_distributed_amd.models import GPT, GPTConfig
+    from mingpt_distributed_amd.parallel import dist as D
+    from mingpt_distributed_amd.trainer import StepEngine
+
+    info = D.init_distributed(device="cuda")
+    if info.world_size != a.gpus:
+        if info.rank == 0:
+            print(f"warning: --gpus {a.gpus} but WORLD_SIZE={info.world_size}; using WORLD_SIZE",
+                  file=sys.stderr)
+    N = info.world_size
+    torch.manual_seed(1234 + info.rank)
+    cfg = GPTConfig(model_type=a.model, vocab_size=50257, block_size=a.seq, embed_drop=a.dropout,
+                    resid_drop=a.dropout, attn_drop=a.dropout)
+    torch.manual_seed(1234)  # identical init on every rank (the engine also broadcasts rank 0)
+    model = GPT(cfg, verbose=info.rank == 0)
+    eng = StepEngine(model, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, grad_clip=1.0,
+                     bucket_mb=a.bucket_mb)
+    g = torch.Generator(device=eng.device).manual_seed(99 + info.rank)
+    nb = 4
+    xs = [torch.randint(0, 50257, (a.batch, a.seq), device=eng.device, generator=g) for _ in range(nb)]
+    ys = [torch.randint(0, 50257, (a.batch, a.seq), device=eng.device, generator=g) for _ in range(nb)]
+
+    for i in range(a.warmup):
+        loss = eng.train_step([(xs[i % nb], ys[i % nb])])
+    D.barrier()
+    torch.cuda.synchronize()
+    prof = None
+    if a.profile and info.rank == 0:
+        prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
+                                                  torch.profiler.ProfilerActivity.CUDA])
+        prof.__enter__()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss = eng.train_step([(xs[i % nb], ys[i % nb])])
+    torch.cuda.synchronize()
+    D.barrier()
+    dt = time.perf_counter() - t0
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        os.makedirs(a.profile, exist_ok=True)
+        prof.export_chrome_trace(os.path.join(a.profile, "trace.json"))
+        with open(os.path.join(a.profile, "summary.txt"), "w") as f:
+            f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+    dt = D.all_reduce_max(dt, eng.device)
+    loss_v = D.all_reduce_mean(loss.float()).item()
+    tokens = a.batch * a.seq * a.steps * N
+    value = tokens / dt
+    if info.rank == 0:
+        out = {
+            "metric": "tokens/sec (whole node), GPT-2 124M seq1024 bf16" if a.model == "gpt2"
+            else f"tokens/sec (whole node), {a.model} seq{a.seq} bf16",
+            "value": round(value, 1),
+            "unit": "tokens/s",
+            "n_gpus": N,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / (BASELINE_TOK_S_PER_GPU * N), 3) if a.model == "gpt2" and a.seq == 1024 else None,
+            "dtype": "bf16",
+            "data": "synthetic (random tokens, random-init weights)",
+            "config": {"model": a.model, "global_batch": a.batch * N, "seq_len": a.seq,
+                       "parallelism": f"dp{N}", "micro_batch_per_gpu": a.batch, "dropout": a.dropout,
+                       "bucket_mb": a.bucket_mb},
+            "loss": round(loss_v, 4),
+            "max_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2),
+        }
+        print(json.dumps(out), flush=True)
+    D.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -53,7 +53,7 @@ std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const at::Tensor& w, 
 
 at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
                          const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& dw,
-                         const at::Tensor& db) {
+                         const at::Tensor& db, const c10::optional<at::Tensor>& dres) {
   CHECK_BF16(dy); CHECK_BF16(x); CHECK_BF16(w); CHECK_F32(mean); CHECK_F32(rstd);
   CHECK_F32(dw); CHECK_F32(db); CHECK_CONTIG(dy); CHECK_CONTIG(x);
   const int64_t D = x.size(-1), M = x.numel() / D;
@@ -63,7 +63,11 @@ at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Te
   auto dx = at::empty_like(x);
   auto ws = at::empty({(int64_t)(mg::layernorm_bwd_workspace((int)M, (int)D) / 4)},
                       x.options().dtype(at::kFloat));
-  mg::layernorm_bwd(bp(dy), bp(x), bp(w), fp(mean), fp(rstd), bp(dx), fp(dw), fp(db), fp(ws),
+  if (dres.has_value() && dres->defined()) {
+    CHECK_BF16(*dres); CHECK_CONTIG(*dres);
+    TORCH_CHECK(dres->numel() == x.numel(), "layernorm_bwd: dres shape");
+  }
+  mg::layernorm_bwd(bp(dy), bp(x), bp(w), fp(mean), fp(rstd), bp_opt(dres), bp(dx), fp(dw), fp(db), fp(ws),
                     (int)M, (int)D, cur_stream());
   return dx;
 }
@@ -268,6 +272,53 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
            cur_stream());
 }
 
+// ------------------------------------------------------------------------------- attention
+std::vector<at::Tensor> attention_fwd(const at::Tensor& qkv, int64_t B, int64_t T, int64_t H,
+                                      double p, int64_t seed) {
+  CHECK_BF16(qkv); CHECK_CONTIG(qkv);
+  const int64_t D3 = qkv.size(-1), D = D3 / 3, hd = D / H;
+  TORCH_CHECK(D3 == 3 * D && D == H * hd && qkv.numel() == B * T * D3, "attention: qkv shape");
+  TORCH_CHECK(hd % 8 == 0 && hd <= 64, "attention: head dim must be a multiple of 8 and <= 64");
+  DevGuard g(qkv.device());
+  auto out = at::empty({B * T, D}, qkv.options());
+  auto lse = at::empty({B * H * T}, qkv.options().dtype(at::kFloat));
+  mg::attention_fwd(bp(qkv), bp(out), fp(lse), (int)B, (int)T, (int)H, (int)hd, (float)p,
+                    (uint64_t)seed, cur_stream());
+  return {out, lse};
+}
+
+at::Tensor attention_bwd(const at::Tensor& qkv, const at::Tensor& out, const at::Tensor& dout,
+                         const at::Tensor& lse, int64_t B, int64_t T, int64_t H, double p,
+                         int64_t seed) {
+  CHECK_BF16(qkv); CHECK_BF16(out); CHECK_BF16(dout); CHECK_F32(lse);
+  CHECK_CONTIG(qkv); CHECK_CONTIG(out); CHECK_CONTIG(dout);
+  const int64_t D3 = qkv.size(-1), D = D3 / 3, hd = D / H;
+  TORCH_CHECK(qkv.numel() == B * T * D3 && out.numel() == B * T * D && dout.numel() == B * T * D &&
+              lse.numel() == B * H * T && hd % 8 == 0 && hd <= 64, "attention_bwd: shape mismatch");
+  DevGuard g(qkv.device());
+  auto dqkv = at::empty_like(qkv);
+  auto opts = qkv.options().dtype(at::kFloat);
+  auto delta = at::empty({B * H * T}, opts);
+  auto dq = at::empty({B * T * D}, opts);
+  mg::attention_bwd(bp(qkv), bp(out), bp(dout), fp(lse), fp(delta), fp(dq), bp(dqkv), (int)B,
+                    (int)T, (int)H, (int)hd, (float)p, (uint64_t)seed, cur_stream());
+  return dqkv;
+}
+
+at::Tensor attention_decode(const at::Tensor& qkv_new, const at::Tensor& cache, int64_t H,
+                            int64_t pos) {
+  CHECK_BF16(qkv_new); CHECK_BF16(cache); CHECK_CONTIG(qkv_new); CHECK_CONTIG(cache);
+  TORCH_CHECK(cache.dim() == 3, "cache must be [B, Tmax, 3D]");
+  const int64_t B = cache.size(0), Tmax = cache.size(1), D3 = cache.size(2), D = D3 / 3;
+  TORCH_CHECK(qkv_new.numel() == B * D3 && D % H == 0, "attention_decode: shape mismatch");
+  TORCH_CHECK(pos >= 0 && pos < Tmax && (D / H) % 8 == 0, "attention_decode: pos / head dim");
+  DevGuard g(cache.device());
+  auto out = at::empty({B, D}, cache.options());
+  mg::attention_decode(bp(qkv_new), bp(cache), bp(out), (int)B, (int)H, (int)(D / H), Tmax, (int)pos,
+                       cur_stream());
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -287,4 +338,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dropout_bwd", &dropout_bwd);
   m.def("bias_grad", &bias_grad);
   m.def("gemm", &gemm);
+  m.def("attention_fwd", &attention_fwd);
+  m.def("attention_bwd", &attention_bwd);
+  m.def("attention_decode", &attention_decode);
 }

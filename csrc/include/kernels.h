@@ -13,8 +13,8 @@ typedef uint16_t bf16_t;
 void layernorm_fwd(const bf16_t* x, const bf16_t* w, const bf16_t* b, bf16_t* y, float* mean,
                    float* rstd, int M, int D, float eps, hipStream_t stream);
 void layernorm_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const float* mean,
-                   const float* rstd, bf16_t* dx, float* dw, float* db, float* workspace, int M,
-                   int D, hipStream_t stream);
+                   const float* rstd, const bf16_t* dres, bf16_t* dx, float* dw, float* db,
+                   float* workspace, int M, int D, hipStream_t stream);
 size_t layernorm_bwd_workspace(int M, int D);
 
 // embedding.hip
@@ -53,5 +53,17 @@ void bias_grad(const bf16_t* dy, float* db, long M, int N, hipStream_t stream);
 void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long lda, long ldb,
           long ldc, int M, int N, int K, int a_ext, int b_ext, int ka, int kb, const bf16_t* bias,
           bf16_t* aux, const bf16_t* resid, float p, uint64_t seed, hipStream_t stream);
+
+// attention.hip -- causal flash attention, hd <= 64; qkv [B*T, 3D], out [B*T, D], lse [B*H*T]
+void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, int B, int T, int H, int hd, float p,
+                   uint64_t seed, hipStream_t stream);
+// delta [B*H*T] and dq [B*T*D] fp32 are workspaces; writes all three slots of dqkv
+void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse,
+                   float* delta, float* dq, bf16_t* dqkv, int B, int T, int H, int hd, float p,
+                   uint64_t seed, hipStream_t stream);
+
+// one decode step: appends K/V of qkv_new [B, 3D] at row pos of cache [B, Tmax, 3D]; out [B, D]
+void attention_decode(const bf16_t* qkv_new, bf16_t* cache, bf16_t* out, int B, int H, int hd,
+                      long Tmax, int pos, hipStream_t stream);
 
 }  // namespace mg

@@ -1,0 +1,613 @@
+// Causal flash attention, forward and backward, for gfx950 (CDNA4, MI355X).
+//
+// Replaces the reference's nn.MultiheadAttention math path
+// (/root/reference/mingpt/model.py:147-165: in-proj split, q*scale, baddbmm with the [T,T] mask,
+// softmax, dropout, bmm PV, plus the discarded head-averaged weights) with a true causal kernel
+// that never materialises [T, T] (fixes D4: the reference's additive 0/1 mask was not causal).
+//
+// I/O layout: qkv [B*T, 3*D] bf16 straight from the c_attn GEMM (q | k | v, head h at columns
+// h*hd..), out [B*T, D] bf16, lse [B*H*T] fp32 (log2 domain).  hd <= 64 (every GPT-2 size is 64;
+// gpt-mini/micro are 32, gpt-nano 16): tiles are 64 wide and zero-padded.
+//
+// Forward (FA2 structure, MI355X mapping):
+//  * workgroup = 4 waves = 128 queries of one (b, h); each wave owns 32 queries.
+//  * Q fragments live in VGPRs for the whole kernel; K/V tiles of 64 keys are staged through LDS
+//    (double buffer, loads for tile t+1 issued before the MFMAs of tile t).
+//  * S^T = K Q^T with v_mfma_f32_32x32x16_bf16 ("swapped" operands): the query is on the lane,
+//    so the softmax row statistics are lane-local (one xor-32 shuffle joins the two halves).
+//  * P is converted to bf16 in registers and used directly as the B operand of O^T = V^T P^T
+//    (guide §3 "accumulator tile as the next MFMA's operand"); V^T fragments come from LDS with
+//    ds_read_b64_tr_b16 in the matching permuted key order.  O^T keeps queries on the lane too,
+//    so the online-softmax rescale is a per-lane multiply.
+//  * LDS images use a 128-B-row XOR swizzle that is bank-conflict-free for both the row reads
+//    (ds_read_b128) and the transposed reads (found by exhaustive search, see PERF.md).
+//  * heaviest (last) query blocks are launched first; fully-masked K tiles are skipped per wave.
+//
+// Backward (key-block parallel):
+//  * workgroup = 4 waves = 128 keys of one (b, h); each wave keeps its 32 keys' K and V fragments
+//    in VGPRs and dK^T/dV^T accumulators (keys on the lane) across the whole query sweep.
+//  * per 64-query tile (Q, dO, lse, delta staged in LDS): S and dP with the key on the lane, P and
+//    dS in registers feed dV^T += dO^T P and dK^T += Q^T dS directly (tr-reads of Q/dO);
+//    dS is transposed once through LDS for dQ = dS K, the 4 waves' dQ partials are summed with
+//    LDS float atomics, then one fp32 global atomic per element per workgroup.
+//  * attention dropout: Philox mask regenerated from (seed, b, h, q, key) in both passes.
+#include "common.h"
+#include "kernels.h"
+
+using namespace mg;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int HD = 64;        // tile head dim
+constexpr int ROWB = HD * 2;  // 128-B LDS rows
+constexpr float kNegBig = -1e30f;
+
+// conflict-free for ds_read_b128 (32-row operand) and both ds_read_b64_tr_b16 patterns
+MG_DEVICE int swz(int r) { return ((r >> 1) & 3) | ((((r >> 1) ^ (r >> 3)) & 1) << 2); }
+MG_DEVICE int lds_off(int row, int ch) { return row * ROWB + ((ch ^ swz(row)) << 4); }
+
+struct AttnArgs {
+  const bf16_t* qkv;
+  bf16_t* out;
+  float* lse;          // [B*H*T], log2 domain
+  const bf16_t* dout;  // bwd
+  const float* delta;  // bwd [B*H*T]
+  float* dq;           // bwd [B*T, D] fp32 accumulator
+  bf16_t* dqkv;        // bwd [B*T, 3D]
+  int B, T, H, hd, D;
+  float scale_log2;    // log2(e) / sqrt(hd)
+  uint64_t seed;
+  uint32_t thr;
+  float dscale;        // 1 / (1 - p)
+};
+
+MG_DEVICE bf16x8 lds_row_frag(const char* base, int row, int ch) {
+  return *reinterpret_cast<const bf16x8*>(base + lds_off(row, ch));
+}
+
+// Transposed 8-element fragment: column col of rows r0..r0+3 (elements 0..3) and r1..r1+3 (4..7).
+// Lane (in its 16-lane group) 4q+p addresses row r?+q, columns colbase+4p..+3.
+MG_DEVICE bf16x8 lds_tr_frag(const char* base, int r0, int r1, int colbase, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3;
+  const int col = colbase + 4 * p;
+  const int ra = r0 + q, rb = r1 + q;
+  const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)(base + lds_off(ra, col >> 3) + (col & 7) * 2));
+  const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)(base + lds_off(rb, col >> 3) + (col & 7) * 2));
+  const s16x8 v = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+MG_DEVICE bf16x8 pack_frag(const f32x16& a, int s) {
+  s16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(a[8 * s + j]);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// stage a [64 rows][64 cols] bf16 tile (rows r0.., column offset col0 in a row-major matrix with
+// leading dimension ld) into registers: 512 chunks of 16 B, 2 per thread.
+MG_DEVICE void load64(uint4 (&reg)[2], const bf16_t* base, long ld, int r0, int rows, int hd) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = threadIdx.x + 256 * i;
+    const int row = idx >> 3, ch = idx & 7;
+    const int r = r0 + row;
+    reg[i] = (r < rows && ch * 8 < hd) ? ld16(base + (long)r * ld + ch * 8) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+MG_DEVICE void store64(char* lds, const uint4 (&reg)[2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = threadIdx.x + 256 * i;
+    *reinterpret_cast<uint4*>(lds + lds_off(idx >> 3, idx & 7)) = reg[i];
+  }
+}
+
+// Philox counter of the attention-dropout mask: row = (b*H + h)*T + q, 4 keys per counter.
+MG_DEVICE uint64_t drop_ctr(uint64_t row, int T, int key) {
+  return row * (uint64_t)((T + 3) >> 2) + (uint64_t)(key >> 2);
+}
+
+// =============================================================================== forward
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * 64 * ROWB];  // K0 V0 K1 V1
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h32 = lane >> 5, l32 = lane & 31;
+  const int nqb = (a.T + 127) / 128;
+  const int bh = blockIdx.x % (a.B * a.H);
+  const int qb = nqb - 1 - blockIdx.x / (a.B * a.H);  // heaviest blocks first
+  const int b = bh / a.H, hh = bh % a.H;
+  const int q0 = qb * 128;
+  const long ld = 3L * a.D;
+  const bf16_t* Qg = a.qkv + (long)b * a.T * ld + hh * a.hd;
+  const bf16_t* Kg = Qg + a.D;
+  const bf16_t* Vg = Qg + 2 * a.D;
+
+  const int myq = q0 + 32 * w + l32;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int d = ks * 16 + 8 * h32;
+    uint4 u = (myq < a.T && d < a.hd) ? ld16(Qg + (long)myq * ld + d) : make_uint4(0, 0, 0, 0);
+    qf[ks] = __builtin_bit_cast(bf16x8, u);
+  }
+  const int nks = (a.hd + 15) / 16;
+
+  f32x16 o0 = {0}, o1 = {0};
+  float m = kNegBig, l = 0.f;
+  const int kend = min(a.T, q0 + 128);
+  const int ntiles = (kend + 63) / 64;
+  const int wave_qmax = q0 + 32 * w + 31;
+  const uint64_t drop_row = (uint64_t)bh * a.T + myq;
+
+  uint4 rk[2], rv[2];
+  load64(rk, Kg, ld, 0, a.T, a.hd);
+  load64(rv, Vg, ld, 0, a.T, a.hd);
+  store64(smem, rk);
+  store64(smem + 64 * ROWB, rv);
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const char* sk = smem + (t & 1) * 2 * 64 * ROWB;
+    const char* sv = sk + 64 * ROWB;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      load64(rk, Kg, ld, (t + 1) * 64, a.T, a.hd);
+      load64(rv, Vg, ld, (t + 1) * 64, a.T, a.hd);
+    }
+    const int k0 = t * 64;
+    if (k0 <= wave_qmax) {
+      f32x16 s[2];
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        s[sub] = f32x16{0};
+        for (int ks = 0; ks < nks; ++ks)
+          s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              lds_row_frag(sk, sub * 32 + l32, ks * 2 + h32), qf[ks], s[sub], 0, 0, 0);
+      }
+      // scale + mask, row max
+      const bool diag = k0 + 63 > q0 + 32 * w;
+      float mx = kNegBig;
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + sub * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+          float v = s[sub][r] * a.scale_log2;
+          if ((diag && key > myq) || key >= a.T) v = kNegBig;
+          s[sub][r] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m, mx);
+      const float alpha = exp2f(m - mn);
+      m = mn;
+      float rs = 0.f;
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = exp2f(s[sub][r] - mn);
+          s[sub][r] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 32, 64);
+      l = l * alpha + rs;
+      o0 *= alpha;
+      o1 *= alpha;
+      if (a.thr) {  // attention dropout on P (for O only; l uses the undropped P)
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int key = k0 + sub * 32 + 8 * g + 4 * h32;
+            const uint4 rnd = rand4(a.seed, drop_ctr(drop_row, a.T, key));
+            const uint32_t rr[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s[sub][4 * g + j] = rr[j] >= a.thr ? s[sub][4 * g + j] * a.dscale : 0.f;
+          }
+      }
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const bf16x8 pf = pack_frag(s[sub], st);
+          const int r0 = sub * 32 + 16 * st + 4 * h32;
+          const int cb = 16 * ((lane >> 4) & 1);
+          o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sv, r0, r0 + 8, cb, lane), pf, o0, 0, 0, 0);
+          if (a.hd > 32)
+            o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sv, r0, r0 + 8, 32 + cb, lane), pf, o1, 0, 0, 0);
+        }
+    }
+    if (more) {
+      char* dst = smem + ((t + 1) & 1) * 2 * 64 * ROWB;
+      store64(dst, rk);
+      store64(dst + 64 * ROWB, rv);
+    }
+    __syncthreads();
+  }
+
+  if (myq < a.T) {
+    const float inv = 1.f / l;
+    if (h32 == 0) a.lse[(long)bh * a.T + myq] = m + log2f(l);
+    bf16_t* orow = a.out + ((long)b * a.T + myq) * a.D + hh * a.hd;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 8 * g + 4 * h32;
+      if (d < a.hd)
+        *reinterpret_cast<uint2*>(orow + d) =
+            make_uint2(pack2(o0[4 * g] * inv, o0[4 * g + 1] * inv), pack2(o0[4 * g + 2] * inv, o0[4 * g + 3] * inv));
+      if (32 + d < a.hd)
+        *reinterpret_cast<uint2*>(orow + 32 + d) =
+            make_uint2(pack2(o1[4 * g] * inv, o1[4 * g + 1] * inv), pack2(o1[4 * g + 2] * inv, o1[4 * g + 3] * inv));
+    }
+  }
+}
+
+// =============================================================================== backward
+// delta[bh*T + t] = sum_d dO * O ; also zero dq
+__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restrict__ dout,
+                                                           const bf16_t* __restrict__ out,
+                                                           float* __restrict__ delta, int B, int T,
+                                                           int H, int hd, int D) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;  // over B*H*T
+  if (i >= (long)B * H * T) return;
+  const int t = (int)(i % T);
+  const long bh = i / T;
+  const int b = (int)(bh / H), hh = (int)(bh % H);
+  const long off = ((long)b * T + t) * D + hh * hd;
+  float s = 0.f;
+  for (int d = 0; d < hd; d += 8) {
+    float x[8], y[8];
+    unpack8(ld16(dout + off + d), x);
+    unpack8(ld16(out + off + d), y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += x[j] * y[j];
+  }
+  delta[i] = s;
+}
+
+constexpr int BQ = 64;  // queries per bwd tile
+// LDS: Q[64 rows], dO[64 rows] (single buffer; next tile prefetched in VGPRs), K[128 rows], dS^T per wave [32 keys][64 q] bf16,
+//      dQ acc [64][64] f32, lse/delta [2][64] f32
+constexpr int BWD_Q_OFF = 0;
+constexpr int BWD_DO_OFF = BWD_Q_OFF + BQ * ROWB;
+constexpr int BWD_K_OFF = BWD_DO_OFF + BQ * ROWB;
+constexpr int BWD_DS_OFF = BWD_K_OFF + 128 * ROWB;
+constexpr int BWD_DQ_OFF = BWD_DS_OFF + 4 * 32 * BQ * 2;
+constexpr int BWD_LD_OFF = BWD_DQ_OFF + BQ * HD * 4;
+constexpr int BWD_SMEM = BWD_LD_OFF + 2 * BQ * 4;  // 64.5 KiB -> 2 workgroups per CU
+
+// dS^T image per wave: [32 keys][64 q] bf16, 128-B rows, same swizzle (row = key)
+__global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h32 = lane >> 5, l32 = lane & 31;
+  const int nkb = (a.T + 127) / 128;
+  const int bh = blockIdx.x % (a.B * a.H);
+  const int kb = blockIdx.x / (a.B * a.H);  // light-to-heavy is fine: every block sweeps to T
+  const int b = bh / a.H, hh = bh % a.H;
+  const int kb0 = kb * 128;
+  const long ld = 3L * a.D;
+  const bf16_t* Qg = a.qkv + (long)b * a.T * ld + hh * a.hd;
+  const bf16_t* Kg = Qg + a.D;
+  const bf16_t* Vg = Qg + 2 * a.D;
+  const bf16_t* dOg = a.dout + (long)b * a.T * a.D + hh * a.hd;
+  const float* lseg = a.lse + (long)bh * a.T;
+  const float* dlg = a.delta + (long)bh * a.T;
+  const int mykey = kb0 + 32 * w + l32;
+  const int nks = (a.hd + 15) / 16;
+
+  char* sK = smem + BWD_K_OFF;
+  char* sdS = smem + BWD_DS_OFF + w * 32 * ROWB;
+  float* sdQ = reinterpret_cast<float*>(smem + BWD_DQ_OFF);
+  float* sLD = reinterpret_cast<float*>(smem + BWD_LD_OFF);
+
+  // K block -> LDS (for dQ), K/V fragments of this wave's keys -> VGPRs
+  {
+    uint4 r0[2], r1[2];
+    load64(r0, Kg, ld, kb0, a.T, a.hd);
+    load64(r1, Kg, ld, kb0 + 64, a.T, a.hd);
+    store64(sK, r0);
+    store64(sK + 64 * ROWB, r1);
+  }
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int d = ks * 16 + 8 * h32;
+    const bool ok = mykey < a.T && d < a.hd;
+    kf[ks] = __builtin_bit_cast(bf16x8, ok ? ld16(Kg + (long)mykey * ld + d) : make_uint4(0, 0, 0, 0));
+    vf[ks] = __builtin_bit_cast(bf16x8, ok ? ld16(Vg + (long)mykey * ld + d) : make_uint4(0, 0, 0, 0));
+  }
+  for (int i = threadIdx.x; i < BQ * HD; i += 256) sdQ[i] = 0.f;
+
+  f32x16 dk0 = {0}, dk1 = {0}, dv0 = {0}, dv1 = {0};
+  const int qt0 = kb0 / BQ;
+  const int nqt = (a.T + BQ - 1) / BQ;
+  const int wave_kmin = kb0 + 32 * w;
+
+  uint4 rq[2], rd[2];
+  float rl = 0.f, rdl = 0.f;
+  auto issue = [&](int qt) {
+    load64(rq, Qg, ld, qt * BQ, a.T, a.hd);
+    load64(rd, dOg, a.D, qt * BQ, a.T, a.hd);
+    if (threadIdx.x < BQ) {
+      const int q = qt * BQ + threadIdx.x;
+      rl = q < a.T ? lseg[q] : 0.f;
+      rdl = q < a.T ? dlg[q] : 0.f;
+    }
+  };
+  auto commit = [&]() {
+    store64(smem + BWD_Q_OFF, rq);
+    store64(smem + BWD_DO_OFF, rd);
+    if (threadIdx.x < BQ) {
+      sLD[threadIdx.x] = rl;
+      sLD[BQ + threadIdx.x] = rdl;
+    }
+  };
+  issue(qt0);
+  commit();
+  __syncthreads();
+
+  for (int qt = qt0; qt < nqt; ++qt) {
+    const char* sQ = smem + BWD_Q_OFF;
+    const char* sdO = smem + BWD_DO_OFF;
+    const float* sL = sLD;
+    // opaque per-iteration lane id: keeps the (loop-invariant) LDS addresses from being hoisted
+    // into dozens of live VGPRs; they are recomputed with a few VALU ops instead.
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
+    const int h32 = lane >> 5, l32 = lane & 31;
+    const bool more = qt + 1 < nqt;
+    if (more) issue(qt + 1);
+    const int qbase = qt * BQ;
+    const bool active = qbase + BQ - 1 >= wave_kmin && wave_kmin < a.T;
+    if (active) {
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        const int qsub0 = qbase + qs * 32;
+        if (qsub0 + 31 < wave_kmin) {  // all queries of this subtile precede every key: P = 0
+          // still must write zeros into the dS^T image for the dQ product
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<uint2*>(sdS + lds_off(l32, (qs * 32 + 8 * g + 4 * h32) >> 3) +
+                                      ((qs * 32 + 8 * g + 4 * h32) & 7) * 2) = make_uint2(0, 0);
+          continue;
+        }
+        f32x16 s = {0}, dp = {0};
+        for (int ks = 0; ks < nks; ++ks) {
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_frag(sQ, qs * 32 + l32, ks * 2 + h32), kf[ks], s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_frag(sdO, qs * 32 + l32, ks * 2 + h32), vf[ks], dp, 0, 0, 0);
+        }
+        // rows of s/dp = queries qs*32 + (r&3) + 8(r>>2) + 4*h32 ; col = key (lane).
+        // In place: s <- dropped P (for dV), dp <- dS.
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ql = qs * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+          const int q = qbase + ql;
+          float p = exp2f(s[r] * a.scale_log2 - sL[ql]);
+          if (mykey > q || q >= a.T || mykey >= a.T) p = 0.f;
+          float dpv = dp[r];
+          float pdrop = p;
+          if (a.thr) {
+            const uint4 rnd = rand4(a.seed, drop_ctr((uint64_t)bh * a.T + q, a.T, mykey));
+            const uint32_t sel = (mykey & 3) == 0 ? rnd.x : (mykey & 3) == 1 ? rnd.y : (mykey & 3) == 2 ? rnd.z : rnd.w;
+            const float z = sel >= a.thr ? a.dscale : 0.f;
+            pdrop = p * z;
+            dpv *= z;
+          }
+          s[r] = pdrop;
+          dp[r] = p * (dpv - sL[BQ + ql]);
+        }
+        // dV^T += dO^T P ; dK^T += Q^T dS   (sum over this subtile's 32 queries)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const bf16x8 pf = pack_frag(s, st);
+          const bf16x8 dsf = pack_frag(dp, st);
+          const int r0 = qs * 32 + 16 * st + 4 * h32;
+          const int cb = 16 * ((lane >> 4) & 1);
+          dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sdO, r0, r0 + 8, cb, lane), pf, dv0, 0, 0, 0);
+          dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sQ, r0, r0 + 8, cb, lane), dsf, dk0, 0, 0, 0);
+          if (a.hd > 32) {
+            dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sdO, r0, r0 + 8, 32 + cb, lane), pf, dv1, 0, 0, 0);
+            dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sQ, r0, r0 + 8, 32 + cb, lane), dsf, dk1, 0, 0, 0);
+          }
+        }
+        // dS^T image [key = lane][q]: 4 consecutive q per 8-byte write
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int qc = qs * 32 + 8 * g + 4 * h32;
+          *reinterpret_cast<uint2*>(sdS + lds_off(l32, qc >> 3) + (qc & 7) * 2) =
+              make_uint2(pack2(dp[4 * g], dp[4 * g + 1]), pack2(dp[4 * g + 2], dp[4 * g + 3]));
+        }
+      }
+      // dQ partial = dS K over this wave's 32 keys: A = dS [q x key] (tr-read of dS^T image),
+      // B = K [key x d] (tr-read of the K block image); natural k order on both sides.
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        f32x16 dq0 = {0}, dq1 = {0};
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {  // 32 keys = 2 k-steps of 16
+          const int kr0 = kk * 16 + 8 * h32;
+          const bf16x8 af = lds_tr_frag(sdS, kr0, kr0 + 4, qs * 32 + 16 * ((lane >> 4) & 1), lane);
+          const int krow = 32 * w + kr0;
+          const int cb = 16 * ((lane >> 4) & 1);
+          dq0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, lds_tr_frag(sK, krow, krow + 4, cb, lane), dq0, 0, 0, 0);
+          if (a.hd > 32)
+            dq1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, lds_tr_frag(sK, krow, krow + 4, 32 + cb, lane), dq1, 0, 0, 0);
+        }
+        // dq[q][d]: col = d (lane), rows = q
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ql = qs * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+          atomicAdd(&sdQ[ql * HD + l32], dq0[r]);
+          if (a.hd > 32) atomicAdd(&sdQ[ql * HD + 32 + l32], dq1[r]);
+        }
+      }
+    }
+    __syncthreads();  // every wave is done with the Q/dO tile and has added its dQ partial
+    // flush the summed dQ tile to global (fp32 atomics, 64 contiguous floats per wave-instruction)
+    for (int i = threadIdx.x; i < BQ * HD; i += 256) {
+      const int ql = i / HD, d = i % HD;
+      const int q = qbase + ql;
+      const float v = sdQ[i];
+      sdQ[i] = 0.f;
+      if (q < a.T && d < a.hd && v != 0.f) atomicAdd(a.dq + ((long)b * a.T + q) * a.D + hh * a.hd + d, v);
+    }
+    if (more) commit();
+    __syncthreads();
+  }
+
+  // dK (scaled), dV -> dqkv K / V slots ; lane holds d = (r&3) + 8(r>>2) + 4*h32 (+32), key = lane
+  if (mykey < a.T) {
+    const float sc = a.scale_log2 * 0.6931471805599453f;  // 1/sqrt(hd)
+    bf16_t* krow = a.dqkv + ((long)b * a.T + mykey) * ld + a.D + hh * a.hd;
+    bf16_t* vrow = krow + a.D;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 8 * g + 4 * h32;
+      if (d < a.hd) {
+        *reinterpret_cast<uint2*>(krow + d) = make_uint2(pack2(dk0[4 * g] * sc, dk0[4 * g + 1] * sc),
+                                                         pack2(dk0[4 * g + 2] * sc, dk0[4 * g + 3] * sc));
+        *reinterpret_cast<uint2*>(vrow + d) = make_uint2(pack2(dv0[4 * g], dv0[4 * g + 1]),
+                                                         pack2(dv0[4 * g + 2], dv0[4 * g + 3]));
+      }
+      if (32 + d < a.hd) {
+        *reinterpret_cast<uint2*>(krow + 32 + d) = make_uint2(pack2(dk1[4 * g] * sc, dk1[4 * g + 1] * sc),
+                                                              pack2(dk1[4 * g + 2] * sc, dk1[4 * g + 3] * sc));
+        *reinterpret_cast<uint2*>(vrow + 32 + d) = make_uint2(pack2(dv1[4 * g], dv1[4 * g + 1]),
+                                                              pack2(dv1[4 * g + 2], dv1[4 * g + 3]));
+      }
+    }
+  }
+}
+
+// dqkv Q slot = bf16(dq * scale)
+__global__ __launch_bounds__(256) void attn_dq_finalize_kernel(const float* __restrict__ dq,
+                                                               bf16_t* __restrict__ dqkv, long rows,
+                                                               int D, float sc) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;  // over rows * D/8
+  const long n8 = rows * (D / 8);
+  if (i >= n8) return;
+  const long r = i / (D / 8);
+  const int c = (int)(i % (D / 8)) * 8;
+  const float4 x0 = *reinterpret_cast<const float4*>(dq + r * D + c);
+  const float4 x1 = *reinterpret_cast<const float4*>(dq + r * D + c + 4);
+  const float f[8] = {x0.x * sc, x0.y * sc, x0.z * sc, x0.w * sc, x1.x * sc, x1.y * sc, x1.z * sc, x1.w * sc};
+  st16(dqkv + r * 3L * D + c, pack8(f));
+}
+
+// =============================================================================== decode
+// One new query per sequence attending to a KV cache held as qkv rows [B, Tmax, 3D] (the prefill
+// writes its qkv GEMM output straight into it).  Appends this step's K/V at row `pos`, then
+// softmax over keys 0..pos.  grid = B*H, 256 threads; scores live in LDS (Tmax floats).
+__global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restrict__ qkv_new,
+                                                          bf16_t* __restrict__ cache,
+                                                          bf16_t* __restrict__ out, int H, int hd,
+                                                          int D, long Tmax, int pos,
+                                                          float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) float dsm[];  // [64 q][Tmax scores][4*64 acc][8]
+  float* qs = dsm;
+  float* sc = dsm + 64;
+  float* acc = sc + ((Tmax + 3) & ~3L);
+  float* red = acc + 4 * 64;
+  const int b = blockIdx.x / H, hh = blockIdx.x % H;
+  const long ld = 3L * D;
+  const bf16_t* qrow = qkv_new + (long)b * ld + hh * hd;
+  bf16_t* cb = cache + (long)b * Tmax * ld;
+  for (int i = threadIdx.x; i < 2 * hd; i += 256) {
+    const int which = i / hd, d = i % hd;
+    cb[(long)pos * ld + (long)D * (1 + which) + hh * hd + d] = qrow[(long)D * (1 + which) + d];
+  }
+  for (int d = threadIdx.x; d < hd; d += 256) qs[d] = bf2f(qrow[d]);
+  __syncthreads();
+  const int L = pos + 1;
+  float mx = -INFINITY;
+  for (int j = threadIdx.x; j < L; j += 256) {
+    const bf16_t* kr = (j == pos) ? qrow + D : cb + (long)j * ld + D + hh * hd;
+    float s = 0.f;
+    for (int d = 0; d < hd; d += 8) {
+      float k8[8];
+      unpack8(ld16(kr + d), k8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += qs[d + e] * k8[e];
+    }
+    s *= scale_log2;
+    sc[j] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = block_max<4>(mx, red);
+  float sm = 0.f;
+  for (int j = threadIdx.x; j < L; j += 256) {
+    const float p = exp2f(sc[j] - mx);
+    sc[j] = p;
+    sm += p;
+  }
+  sm = block_sum<4>(sm, red + 4);
+  __syncthreads();
+  const int grp = threadIdx.x >> 6, d = threadIdx.x & 63;
+  float o = 0.f;
+  if (d < hd) {
+    for (int j = grp; j < L; j += 4) {
+      const bf16_t* vr = (j == pos) ? qrow + 2 * D : cb + (long)j * ld + 2 * D + hh * hd;
+      o += sc[j] * bf2f(vr[d]);
+    }
+  }
+  acc[grp * 64 + d] = o;
+  __syncthreads();
+  if (threadIdx.x < hd) {
+    const float v = (acc[threadIdx.x] + acc[64 + threadIdx.x] + acc[128 + threadIdx.x] + acc[192 + threadIdx.x]) / sm;
+    out[(long)b * D + hh * hd + threadIdx.x] = f2bf(v);
+  }
+}
+
+}  // namespace
+
+namespace mg {
+
+void attention_decode(const bf16_t* qkv_new, bf16_t* cache, bf16_t* out, int B, int H, int hd,
+                      long Tmax, int pos, hipStream_t stream) {
+  const size_t smem = sizeof(float) * (64 + ((Tmax + 3) & ~3L) + 4 * 64 + 8);
+  attn_decode_kernel<<<B * H, 256, smem, stream>>>(qkv_new, cache, out, H, hd, H * hd, Tmax, pos,
+                                                   1.4426950408889634f / sqrtf((float)hd));
+}
+
+static AttnArgs make_args(int B, int T, int H, int hd, float p, uint64_t seed) {
+  AttnArgs a{};
+  a.B = B; a.T = T; a.H = H; a.hd = hd; a.D = H * hd;
+  a.scale_log2 = 1.4426950408889634f / sqrtf((float)hd);
+  a.seed = seed;
+  a.thr = p > 0.f ? dropout_threshold(p) : 0u;
+  a.dscale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  return a;
+}
+
+void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, int B, int T, int H, int hd, float p,
+                   uint64_t seed, hipStream_t stream) {
+  AttnArgs a = make_args(B, T, H, hd, p, seed);
+  a.qkv = qkv; a.out = out; a.lse = lse;
+  const int grid = cdiv(T, 128) * B * H;
+  attn_fwd_kernel<<<grid, 256, 0, stream>>>(a);
+}
+
+void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse,
+                   float* delta, float* dq, bf16_t* dqkv, int B, int T, int H, int hd, float p,
+                   uint64_t seed, hipStream_t stream) {
+  AttnArgs a = make_args(B, T, H, hd, p, seed);
+  a.qkv = qkv; a.out = dqkv; a.lse = const_cast<float*>(lse); a.dout = dout; a.delta = delta;
+  a.dq = dq; a.dqkv = dqkv;
+  const long bht = (long)B * H * T;
+  attn_bwd_pre_kernel<<<cdiv(bht, 256), 256, 0, stream>>>(dout, out, delta, B, T, H, hd, H * hd);
+  hipMemsetAsync(dq, 0, sizeof(float) * (size_t)B * T * H * hd, stream);
+  const int grid = cdiv(T, 128) * B * H;
+  attn_bwd_kernel<<<grid, 256, BWD_SMEM, stream>>>(a);
+  const long n8 = (long)B * T * (H * hd / 8);
+  attn_dq_finalize_kernel<<<cdiv(n8, 256), 256, 0, stream>>>(dq, dqkv, (long)B * T, H * hd,
+                                                             1.f / sqrtf((float)hd));
+}
+
+}  // namespace mg

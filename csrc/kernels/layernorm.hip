@@ -82,6 +82,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
                                                      const bf16_t* __restrict__ w,
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ rstd,
+                                                     const bf16_t* __restrict__ dres,
                                                      bf16_t* __restrict__ dx,
                                                      float* __restrict__ part, int M, int D) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -128,9 +129,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
     for (int i = 0; i < NV; ++i) {
       const int c = (i * 64 + lane) * 8;
       if (c < D) {
-        float o[8];
+        float o[8], r[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rs * (g[i][j] * wf[i][j] - s1 - xh[i][j] * s2);
+        if (dres) {  // fused residual-branch gradient: dx = LN'(dy) + dres
+          unpack8(ld16(dres + row * D + c), r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += r[j];
+        }
         st16(dxr + c, pack8(o));
       }
     }
@@ -190,11 +196,11 @@ void layernorm_fwd(const bf16_t* x, const bf16_t* w, const bf16_t* b, bf16_t* y,
 }
 
 void layernorm_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const float* mean,
-                   const float* rstd, bf16_t* dx, float* dw, float* db, float* workspace, int M,
-                   int D, hipStream_t stream) {
+                   const float* rstd, const bf16_t* dres, bf16_t* dx, float* dw, float* db,
+                   float* workspace, int M, int D, hipStream_t stream) {
   const int grid = ln_bwd_grid(M);
   const size_t smem = sizeof(float) * 8 * D;
-  MG_LN_DISPATCH(ln_bwd_kernel, dy, x, w, mean, rstd, dx, workspace, M, D);
+  MG_LN_DISPATCH(ln_bwd_kernel, dy, x, w, mean, rstd, dres, dx, workspace, M, D);
   ln_bwd_reduce_kernel<<<cdiv(2 * D, 256), 256, 0, stream>>>(workspace, dw, db, grid, D);
 }
 

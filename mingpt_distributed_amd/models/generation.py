@@ -1,0 +1,163 @@
+"""Autoregressive generation with a KV cache.
+
+Semantics follow the reference ``GPT.generate`` (``/root/reference/mingpt/model.py:322-356``):
+crop the context to ``block_size``, logits of the last position / temperature, optional top-k
+masking to -inf, softmax, multinomial sample or greedy top-1, append.  The reference re-runs the
+full forward over the prefix for every token (defect D32); here the prompt is prefilled once and
+each new token attends to cached keys/values.
+
+GPU path: the prefill runs the gfx950 kernels and keeps each layer's qkv GEMM output as the cache
+([B, Tmax, 3D] rows); each decode step runs LN / GEMM / decode-attention kernels on B rows and
+appends K/V inside the attention kernel.  CPU path: the same algorithm in plain PyTorch.  When the
+sequence outgrows ``block_size`` the window slides and the cache is rebuilt from the cropped
+context (exactly the reference's cropping semantics).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from ..ops import reference as R
+
+
+def _sample(logits, temperature, do_sample, top_k):
+    logits = logits.float() / temperature
+    if top_k is not None:
+        v, _ = torch.topk(logits, min(top_k, logits.size(-1)))
+        logits[logits < v[:, [-1]]] = -float("Inf")
+    probs = F.softmax(logits, dim=-1)
+    if do_sample:
+        return torch.multinomial(probs, num_samples=1)
+    _, idx_next = torch.topk(probs, k=1, dim=-1)
+    return idx_next
+
+
+# ------------------------------------------------------------------------------------ CPU
+class _CpuCache:
+    def __init__(self, model, idx):
+        self.model = model
+        self.k, self.v = [], []
+        self.logits = self._prefill(idx)
+
+    def _prefill(self, idx):
+        m = self.model
+        tr = m.transformer
+        B, T = idx.shape
+        x = tr.wte.weight[idx] + tr.wpe.weight[:T]
+        for blk in tr.h:
+            h = blk.ln_1(x)
+            C = x.shape[-1]
+            q, k, v = F.linear(h, blk.attn.c_attn.weight, blk.attn.c_attn.bias).split(C, dim=2)
+            H = m.config.n_head
+            f = lambda t: t.view(B, T, H, C // H).transpose(1, 2)
+            q, k, v = f(q), f(k), f(v)
+            self.k.append(k)
+            self.v.append(v)
+            y = R.causal_attention(q, k, v, 0.0, False).transpose(1, 2).reshape(B, T, C)
+            x = x + F.linear(y, blk.attn.c_proj.weight, blk.attn.c_proj.bias)
+            x = x + blk.mlp(blk.ln_2(x))
+        return m.lm_head(tr.ln_f(x[:, -1]))
+
+    def step(self, tok, pos):
+        m = self.model
+        tr = m.transformer
+        B = tok.shape[0]
+        x = tr.wte.weight[tok[:, 0]] + tr.wpe.weight[pos]
+        x = x.unsqueeze(1)
+        H = m.config.n_head
+        for i, blk in enumerate(tr.h):
+            h = blk.ln_1(x)
+            C = x.shape[-1]
+            q, k, v = F.linear(h, blk.attn.c_attn.weight, blk.attn.c_attn.bias).split(C, dim=2)
+            f = lambda t: t.view(B, 1, H, C // H).transpose(1, 2)
+            q, k, v = f(q), f(k), f(v)
+            self.k[i] = torch.cat([self.k[i], k], dim=2)
+            self.v[i] = torch.cat([self.v[i], v], dim=2)
+            att = (q @ self.k[i].transpose(-1, -2)) / (C // H) ** 0.5
+            y = (F.softmax(att, dim=-1) @ self.v[i]).transpose(1, 2).reshape(B, 1, C)
+            x = x + F.linear(y, blk.attn.c_proj.weight, blk.attn.c_proj.bias)
+            x = x + blk.mlp(blk.ln_2(x))
+        return m.lm_head(tr.ln_f(x[:, -1]))
+
+
+# ------------------------------------------------------------------------------------ GPU
+class _GpuCache:
+    def __init__(self, model, idx, tmax):
+        from ..ops._ext import ext
+        from ..ops import gemm as G
+        from ..ops.fused import _bf16
+
+        self.C, self.G, self.bf = ext(), G, _bf16
+        self.model = model
+        self.tmax = tmax
+        B, T = idx.shape
+        cfg = model.config
+        D = cfg.n_embed
+        self.caches = [torch.empty(B, tmax, 3 * D, device=idx.device, dtype=torch.bfloat16)
+                       for _ in range(cfg.n_layer)]
+        self.logits = self._run(idx, 0)
+
+    def _run(self, idx, pos0):
+        C, G, bf = self.C, self.G, self.bf
+        m = self.model
+        tr, cfg = m.transformer, m.config
+        B, T = idx.shape
+        D, H, eps = cfg.n_embed, cfg.n_head, cfg.layer_norm_eps
+        wpe = bf(tr.wpe.weight)
+        if pos0 == 0:
+            x = C.embedding_fwd(idx.contiguous(), bf(tr.wte.weight), wpe, 0.0, 0).view(B * T, D)
+        else:  # single token at position pos0
+            x = C.embedding_fwd(idx.contiguous(), bf(tr.wte.weight), wpe[pos0:pos0 + 1].contiguous(),
+                                0.0, 0).view(B * T, D)
+        for i, blk in enumerate(tr.h):
+            a, mm = blk.attn, blk.mlp
+            h, _, _ = C.layernorm_fwd(x, bf(blk.ln_1.weight), bf(blk.ln_1.bias), eps)
+            qkv = G.gemm_nt(h, bf(a.c_attn.weight), bias=bf(a.c_attn.bias), epi="bias")
+            if pos0 == 0:
+                self.caches[i][:, :T].copy_(qkv.view(B, T, 3 * D))
+                y, _ = C.attention_fwd(qkv, B, T, H, 0.0, 0)
+            else:
+                y = C.attention_decode(qkv, self.caches[i], H, pos0)
+            x = G.gemm_nt(y, bf(a.c_proj.weight), bias=bf(a.c_proj.bias), epi="resid", resid=x)
+            h2, _, _ = C.layernorm_fwd(x, bf(blk.ln_2.weight), bf(blk.ln_2.bias), eps)
+            pre = torch.empty((x.shape[0], 4 * D), dtype=torch.bfloat16, device=x.device)
+            u = G.gemm_nt(h2, bf(mm.c_fc.weight), bias=bf(mm.c_fc.bias), epi="gelu", pre_out=pre)
+            x = G.gemm_nt(u, bf(mm.c_proj.weight), bias=bf(mm.c_proj.bias), epi="resid", resid=x)
+        last = x.view(B, T, D)[:, -1].contiguous()
+        hf, _, _ = C.layernorm_fwd(last, bf(tr.ln_f.weight), bf(tr.ln_f.bias), eps)
+        V = cfg.vocab_size
+        logits = G.gemm_nt(hf, bf(m.lm_head.weight), ld=(V + 7) // 8 * 8)
+        return logits[:, :V]
+
+    def step(self, tok, pos):
+        return self._run(tok, pos)
+
+
+@torch.no_grad()
+def generate(model, idx, max_new_tokens: int, temperature: float = 1.0, do_sample: bool = False,
+             top_k: Optional[int] = None, use_cache: bool = True):
+    bs = model.block_size
+    if not use_cache:
+        for _ in range(max_new_tokens):
+            idx_cond = idx if idx.size(1) <= bs else idx[:, -bs:]
+            logits, _ = model(idx_cond)
+            idx = torch.cat((idx, _sample(logits[:, -1, :], temperature, do_sample, top_k)), dim=1)
+        return idx
+    cache = None
+    for _ in range(max_new_tokens):
+        T = idx.size(1)
+        if cache is None or T > bs:
+            idx_cond = idx if T <= bs else idx[:, -bs:]
+            cache = _GpuCache(model, idx_cond, bs) if idx.is_cuda else _CpuCache(model, idx_cond)
+            cache.pos = idx_cond.size(1)
+            logits = cache.logits
+        idx_next = _sample(logits, temperature, do_sample, top_k)
+        idx = torch.cat((idx, idx_next), dim=1)
+        if idx.size(1) > bs:
+            cache = None  # window slides: rebuild from the cropped context next step
+            continue
+        logits = cache.step(idx_next, cache.pos)
+        cache.pos += 1
+    return idx

@@ -1,0 +1,183 @@
+"""GPU execution path: autograd Functions over the gfx950 kernels.
+
+Granularity is chosen for the MI355X, not for module boundaries: one Function per transformer
+block (LN1 -> QKV GEMM+bias -> flash attention -> proj GEMM with fused bias+dropout+residual ->
+LN2 -> FC GEMM with fused bias+GELU -> proj GEMM with fused bias+dropout+residual), one for the
+embedding and one for final-LN + LM head + cross-entropy.  Every GEMM, norm, attention, loss and
+elementwise op is a hand-written HIP kernel; weight gradients are accumulated in fp32 straight
+into ``param.main_grad`` (see ``grads.py``) so the data-parallel engine can all-reduce a bucket
+the moment its last gradient lands.
+
+Reference anchors: block structure ``/root/reference/mingpt/model.py:171-189`` (with D4/D5/D6
+fixed), embedding ``model.py:193-231``, head + loss ``model.py:309-320``.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import gemm as G
+from ._ext import ext
+from .grads import finish, grad_target, note_use
+
+
+def new_seed() -> int:
+    """Dropout seed from torch's CPU generator (reproducible under torch.manual_seed, no GPU sync)."""
+    return int(torch.randint(1, 2 ** 62, (1,)).item())
+
+
+def _bf16(t: torch.Tensor) -> torch.Tensor:
+    return t if t.dtype == torch.bfloat16 else t.to(torch.bfloat16)
+
+
+# ------------------------------------------------------------------------------------ embedding
+class EmbeddingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx, wte, wpe, p):
+        seed = new_seed() if p > 0 else 0
+        out = ext().embedding_fwd(idx.contiguous(), wte, wpe, float(p), seed)
+        ctx.save_for_backward(idx)
+        ctx.params = (wte, wpe)
+        ctx.p, ctx.seed = p, seed
+        note_use(wte)
+        note_use(wpe)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        wte, wpe = ctx.params
+        bte, mte = grad_target(wte)
+        bpe, mpe = grad_target(wpe)
+        ext().embedding_bwd(idx, g.contiguous(), bte, bpe, ctx.p, ctx.seed)
+        return None, finish(wte, bte, mte), finish(wpe, bpe, mpe), None
+
+
+# ------------------------------------------------------------------------------------ block
+class TransformerBlockFn(torch.autograd.Function):
+    """x [M, D] -> x + attn(ln1(x)) -> (+ mlp(ln2(.)))  with every op on a HIP kernel."""
+
+    @staticmethod
+    def forward(ctx, x, ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, wfc, bfc, wp, bp, cfg):
+        B, T, H, p_attn, p_resid, eps = cfg
+        C = ext()
+        seeds = (new_seed() if p_attn > 0 else 0, new_seed() if p_resid > 0 else 0,
+                 new_seed() if p_resid > 0 else 0)
+        h, mean1, rstd1 = C.layernorm_fwd(x, ln1w, ln1b, eps)
+        qkv = G.gemm_nt(h, wqkv, bias=bqkv, epi="bias")
+        y, lse = C.attention_fwd(qkv, B, T, H, float(p_attn), seeds[0])
+        x1 = G.gemm_nt(y, wo, bias=bo, epi="resid", resid=x, p=p_resid, seed=seeds[1])
+        h2, mean2, rstd2 = C.layernorm_fwd(x1, ln2w, ln2b, eps)
+        pre = torch.empty((x.shape[0], wfc.shape[0]), dtype=torch.bfloat16, device=x.device)
+        u = G.gemm_nt(h2, wfc, bias=bfc, epi="gelu", pre_out=pre)
+        x2 = G.gemm_nt(u, wp, bias=bp, epi="resid", resid=x1, p=p_resid, seed=seeds[2])
+        ctx.save_for_backward(x, h, mean1, rstd1, qkv, y, lse, x1, h2, mean2, rstd2, pre, u)
+        ctx.params = (ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, wfc, bfc, wp, bp)
+        ctx.cfg, ctx.seeds = cfg, seeds
+        for prm in ctx.params:
+            note_use(prm)
+        return x2
+
+    @staticmethod
+    def backward(ctx, dx2):
+        B, T, H, p_attn, p_resid, eps = ctx.cfg
+        C = ext()
+        x, h, mean1, rstd1, qkv, y, lse, x1, h2, mean2, rstd2, pre, u = ctx.saved_tensors
+        ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, wfc, bfc, wp, bp = ctx.params
+        dx2 = dx2.contiguous()
+        g = {}
+        for prm in ctx.params:
+            g[id(prm)] = grad_target(prm)
+        # ---- MLP: x2 = x1 + drop(gelu(h2 Wfc^T + bfc) Wp^T + bp)
+        dz = C.dropout_bwd(dx2, p_resid, ctx.seeds[2]) if p_resid > 0 else dx2
+        G.gemm_tn_acc(dz, u, g[id(wp)][0])
+        C.bias_grad(dz, g[id(bp)][0])
+        dpre = G.gemm_nn(dz, wp, epi="gelu_bwd", aux=pre)
+        G.gemm_tn_acc(dpre, h2, g[id(wfc)][0])
+        C.bias_grad(dpre, g[id(bfc)][0])
+        dh2 = G.gemm_nn(dpre, wfc)
+        dx1 = C.layernorm_bwd(dh2, x1, ln2w, mean2, rstd2, g[id(ln2w)][0], g[id(ln2b)][0], dx2)
+        # ---- attention: x1 = x + drop(attn(h Wqkv^T + bqkv) Wo^T + bo)
+        dz = C.dropout_bwd(dx1, p_resid, ctx.seeds[1]) if p_resid > 0 else dx1
+        G.gemm_tn_acc(dz, y, g[id(wo)][0])
+        C.bias_grad(dz, g[id(bo)][0])
+        dy = G.gemm_nn(dz, wo)
+        dqkv = C.attention_bwd(qkv, y, dy, lse, B, T, H, float(p_attn), ctx.seeds[0])
+        G.gemm_tn_acc(dqkv, h, g[id(wqkv)][0])
+        C.bias_grad(dqkv, g[id(bqkv)][0])
+        dh = G.gemm_nn(dqkv, wqkv)
+        dx = C.layernorm_bwd(dh, x, ln1w, mean1, rstd1, g[id(ln1w)][0], g[id(ln1b)][0], dx1)
+        outs = [finish(prm, *g[id(prm)]) for prm in ctx.params]
+        return (dx, *outs, None)
+
+
+# ------------------------------------------------------------------------------------ head + loss
+class HeadLossFn(torch.autograd.Function):
+    """loss = CE(LN_f(x) @ W^T, targets) with padded-vocab logits; returns (logits[M, Vpad], loss)."""
+
+    @staticmethod
+    def forward(ctx, x, lnw, lnb, w, targets, eps):
+        C = ext()
+        V = w.shape[0]
+        ld = (V + 127) // 128 * 128
+        h, mean, rstd = C.layernorm_fwd(x, lnw, lnb, eps)
+        logits = G.gemm_nt(h, w, ld=ld)
+        out, lse = C.xent_fwd(logits, targets, V)
+        ctx.save_for_backward(x, h, mean, rstd, logits, targets, lse, out)
+        ctx.params = (lnw, lnb, w)
+        ctx.eps = eps
+        for prm in ctx.params:
+            note_use(prm)
+        ctx.mark_non_differentiable(logits)
+        return logits, out[0]
+
+    @staticmethod
+    def backward(ctx, _dlogits, dloss):
+        C = ext()
+        x, h, mean, rstd, logits, targets, lse, out = ctx.saved_tensors
+        lnw, lnb, w = ctx.params
+        V = w.shape[0]
+        gscale = dloss.reshape(1).float().contiguous()
+        dlogits = C.xent_bwd(logits, targets, lse, gscale, out, V)
+        del logits
+        bw, mw = grad_target(w)
+        G.gemm_tn_acc(dlogits, h, bw, n_valid=V)
+        dh = G.gemm_nn(dlogits, w)
+        blw, mlw = grad_target(lnw)
+        blb, mlb = grad_target(lnb)
+        dx = C.layernorm_bwd(dh, x, lnw, mean, rstd, blw, blb, None)
+        return dx, finish(lnw, blw, mlw), finish(lnb, blb, mlb), finish(w, bw, mw), None, None
+
+
+class HeadFn(torch.autograd.Function):
+    """logits = LN_f(x) @ W^T (inference / custom-loss path). Gradient flows to x and weights."""
+
+    @staticmethod
+    def forward(ctx, x, lnw, lnb, w, eps):
+        C = ext()
+        V = w.shape[0]
+        ld = (V + 7) // 8 * 8
+        h, mean, rstd = C.layernorm_fwd(x, lnw, lnb, eps)
+        logits = G.gemm_nt(h, w, ld=ld)
+        ctx.save_for_backward(x, h, mean, rstd)
+        ctx.params = (lnw, lnb, w)
+        ctx.eps, ctx.ld = eps, ld
+        for prm in ctx.params:
+            note_use(prm)
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        C = ext()
+        x, h, mean, rstd = ctx.saved_tensors
+        lnw, lnb, w = ctx.params
+        V = w.shape[0]
+        dl = dlogits.contiguous().to(torch.bfloat16)
+        if ctx.ld > V:
+            dl[:, V:] = 0
+        bw, mw = grad_target(w)
+        G.gemm_tn_acc(dl, h, bw, n_valid=V)
+        dh = G.gemm_nn(dl, w)
+        blw, mlw = grad_target(lnw)
+        blb, mlb = grad_target(lnb)
+        dx = C.layernorm_bwd(dh, x, lnw, mean, rstd, blw, blb, None)
+        return dx, finish(lnw, blw, mlw), finish(lnb, blb, mlb), finish(w, bw, mw), None

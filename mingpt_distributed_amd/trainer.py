@@ -1,0 +1,389 @@
+"""Training runtime.
+
+Two front-ends over one step engine:
+
+* :class:`GPTTrainer` / :class:`GPTTrainerConfig` / :class:`ModelSnapshot` -- the reference's
+  epoch-based distributed trainer (``/root/reference/mingpt/trainer.py:21-183``): DP across GPUs,
+  rank-sharded sampler, grad clipping, periodic loss log, test epoch, snapshot save/resume to a
+  local path or ``s3://`` (fsspec reads, boto3 upload).  The reference's defects are fixed:
+  D15-D17 (wrong method/attribute names), D18 (resume re-trained the saved epoch), D19 (snapshot
+  written by every node's local rank 0: now global rank 0, atomic temp+rename), D20
+  (``set_epoch``), D21 (``eval()`` for the test epoch), D22 (grad norm logged), D23 (loss
+  all-reduced before logging, read from the device only every ``log_every`` batches),
+  D25 (runs without torchrun env).
+* :class:`Trainer` -- the upstream-minGPT iteration API the reference README advertises
+  (``get_default_config``, ``add_callback('on_batch_end', fn)``, ``run()``, ``iter_num`` /
+  ``iter_dt`` / ``loss``).
+
+:class:`StepEngine` is the MI355X part: bf16 compute params + fp32 master/grads in flat buffers,
+fused HIP kernels for forward/backward, :class:`DataParallelEngine` overlapping the bucketed
+RCCL all-reduce with backward, :class:`FusedAdamW` (clip + 1/world folded in on the device).
+"""
+from __future__ import annotations
+
+import contextlib
+import io
+import os
+import time
+from collections import defaultdict
+from dataclasses import asdict, dataclass, field
+from typing import Any, Dict, List, Optional
+
+import torch
+from torch.utils.data import DataLoader, Dataset
+
+from .optim import FlatParamStore, FusedAdamW, param_groups
+from .parallel import dist as D
+from .parallel.ddp import DataParallelEngine
+from .parallel.sampler import DistributedSampler, InfiniteRandomSampler
+from .utils.config import CfgNode
+
+
+# ====================================================================================== engine
+class StepEngine:
+    def __init__(self, model: torch.nn.Module, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
+                 weight_decay: float = 0.1, grad_clip: float = 1.0, decay_names=None,
+                 device: Optional[torch.device] = None, bucket_mb: float = 32.0, reduce_dtype=None):
+        if device is None:
+            info = D.info()
+            if info.device.type == "cuda":
+                device = info.device
+            elif torch.cuda.is_available():
+                device = torch.device("cuda", torch.cuda.current_device())
+            else:
+                device = torch.device("cpu")
+        self.device = torch.device(device)
+        self.model = model.to(self.device)
+        if decay_names is None:
+            decay_names, _ = param_groups(model)
+        self.store = FlatParamStore(model, device=self.device)
+        self.opt = FusedAdamW(self.store, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                              decay_names=decay_names, grad_clip=grad_clip or 0.0)
+        self.dp = DataParallelEngine(self.store, bucket_mb=bucket_mb, reduce_dtype=reduce_dtype) \
+            if D.is_initialized() and torch.distributed.get_world_size() > 1 else None
+        self.world = self.dp.world if self.dp else 1
+
+    @classmethod
+    def from_torch_optimizer(cls, model, optimizer: torch.optim.Optimizer, grad_clip: float, **kw):
+        """Adopt the hyper-parameters of a torch AdamW built by ``create_optimizer``."""
+        g0 = optimizer.param_groups[0]
+        names = {id(p): n for n, p in model.named_parameters()}
+        decay = set()
+        wd = 0.0
+        for g in optimizer.param_groups:
+            if g.get("weight_decay", 0.0) > 0:
+                wd = g["weight_decay"]
+                decay |= {names[id(p)] for p in g["params"] if id(p) in names}
+        return cls(model, lr=g0["lr"], betas=g0["betas"], eps=g0.get("eps", 1e-8), weight_decay=wd,
+                   grad_clip=grad_clip, decay_names=decay, **kw)
+
+    @property
+    def lr(self):
+        return self.opt.param_groups[0]["lr"]
+
+    @lr.setter
+    def lr(self, v):
+        self.opt.param_groups[0]["lr"] = v
+
+    def to_device(self, t: torch.Tensor) -> torch.Tensor:
+        return t.to(self.device, non_blocking=True)
+
+    def forward_backward(self, x, y, scale: float = 1.0, sync: bool = True):
+        ctx = self.dp.no_sync() if (self.dp is not None and not sync) else contextlib.nullcontext()
+        with ctx:
+            _, loss = self.model(x, y)
+            (loss * scale if scale != 1.0 else loss).backward()
+            if self.dp is not None:
+                self.dp.finish()
+        return loss.detach()
+
+    def optimizer_step(self):
+        self.opt.step(grad_scale=1.0 / self.world)
+        self.store.zero_grad()
+
+    def train_step(self, batches) -> torch.Tensor:
+        """One optimizer step over a list of (x, y) micro-batches; returns the mean loss (device)."""
+        n = len(batches)
+        total = None
+        for i, (x, y) in enumerate(batches):
+            l = self.forward_backward(self.to_device(x), self.to_device(y), scale=1.0 / n, sync=(i == n - 1))
+            total = l if total is None else total + l
+        self.optimizer_step()
+        return total / n
+
+    @property
+    def grad_norm(self) -> torch.Tensor:
+        return self.opt.grad_norm
+
+    def model_state_dict(self) -> Dict[str, torch.Tensor]:
+        """fp32 CPU state dict (master weights for parameters)."""
+        s = self.store
+        masters = {id(p): s.master[o:o + n].view(p.shape) for p, o, n in zip(s.params, s.offsets, s.numels)}
+        out = {}
+        for k, v in self.model.state_dict(keep_vars=True).items():
+            src = masters.get(id(v), v)
+            out[k] = src.detach().float().cpu().clone() if src.is_floating_point() else src.detach().cpu().clone()
+        return out
+
+    def load_model_state_dict(self, sd: Dict[str, torch.Tensor]):
+        s = self.store
+        named = dict(self.model.named_parameters())
+        for name, p in named.items():
+            if name in sd:
+                i = s.index[id(p)]
+                o, n = s.offsets[i], s.numels[i]
+                s.master[o:o + n].copy_(sd[name].reshape(-1).to(s.master.device, torch.float32))
+        for name, b in self.model.named_buffers():
+            if name in sd:
+                b.copy_(sd[name])
+        s.sync_params_from_master()
+
+
+# ====================================================================================== snapshots
+@dataclass
+class GPTTrainerConfig:
+    max_epochs: Optional[int] = None
+    batch_size: Optional[int] = None
+    learning_rate: Optional[float] = None   # unused, as in the reference (LR lives in OptimizerConfig)
+    grad_norm_clip: Optional[float] = None
+    dl_num_workers: Optional[int] = 0
+    snapshot_path: Optional[str] = None
+    save_every: Optional[int] = 1
+    # extensions
+    log_every: int = 100
+    grad_accum_steps: int = 1
+    max_steps_per_epoch: Optional[int] = None
+    seed: int = 0
+
+
+@dataclass
+class ModelSnapshot:
+    model_state: "Dict[str, torch.Tensor]"
+    optimizer_state: Dict[str, Any]
+    final_epoch: int
+    step: int = 0
+
+
+def _atomic_save(obj, path: str):
+    """Write to ``path.tmp`` then rename: a crash mid-write never leaves a torn snapshot."""
+    import fsspec
+
+    fs, p = fsspec.core.url_to_fs(path)
+    tmp = p + ".tmp"
+    buf = io.BytesIO()
+    torch.save(obj, buf)
+    with fs.open(tmp, "wb") as f:
+        f.write(buf.getvalue())
+    if fs.exists(p):
+        fs.rm(p)
+    fs.mv(tmp, p)
+
+
+class GPTTrainer:
+    """Reference-API distributed trainer (see module docstring)."""
+
+    s3_client_factory = None  # test seam: callable returning an object with upload_fileobj()
+
+    def __init__(self, config: GPTTrainerConfig, model: torch.nn.Module, optimizer: Any,
+                 train_dataset: Dataset, test_dataset: Optional[Dataset] = None):
+        info = D.info() if D.is_initialized() else D.init_distributed()
+        self.local_rank, self.global_rank, self.world = info.local_rank, info.rank, info.world_size
+        self.config = config
+        self.train_dataset, self.test_dataset = train_dataset, test_dataset
+        self.train_loader = self._prepare_dataloader(train_dataset)
+        self.test_loader = self._prepare_dataloader(test_dataset, shuffle=False) if test_dataset else None
+        if self.config.snapshot_path is None:
+            self.config.snapshot_path = "gpt_snapshot.pt"
+        clip = config.grad_norm_clip or 0.0
+        if isinstance(optimizer, torch.optim.Optimizer):
+            self.engine = StepEngine.from_torch_optimizer(model, optimizer, clip)
+        else:
+            self.engine = StepEngine(model, grad_clip=clip)
+        self.model = self.engine.model
+        self.optimizer = self.engine.opt
+        self.save_every = config.save_every or 1
+        self.last_epoch = -1
+        self.step = 0
+        self.history: List[Dict[str, float]] = []
+        self._load_snapshot()
+
+    # ------------------------------------------------------------------ data
+    def _prepare_dataloader(self, dataset: Dataset, shuffle: bool = True):
+        sampler = DistributedSampler(dataset, num_replicas=self.world, rank=self.global_rank,
+                                     shuffle=shuffle, seed=self.config.seed)
+        return DataLoader(dataset, batch_size=self.config.batch_size, sampler=sampler,
+                          pin_memory=torch.cuda.is_available(), shuffle=False,
+                          num_workers=self.config.dl_num_workers or 0, drop_last=True)
+
+    # ------------------------------------------------------------------ snapshots
+    def _snapshot_dict(self, epoch: int) -> Dict[str, Any]:
+        snap = ModelSnapshot(model_state=self.engine.model_state_dict(),
+                             optimizer_state=self.engine.opt.state_dict(), final_epoch=epoch,
+                             step=self.step)
+        return asdict(snap)
+
+    def _upload_snapshot(self, snapshot, dst: str):
+        from urllib.parse import urlparse
+
+        buffer = io.BytesIO()
+        torch.save(snapshot, buffer)
+        buffer.seek(0)
+        u = urlparse(dst, allow_fragments=False)
+        if self.s3_client_factory is not None:
+            client = self.s3_client_factory()
+        else:
+            import boto3  # lazy: only needed for s3:// snapshots
+
+            client = boto3.client("s3")
+        client.upload_fileobj(buffer, u.netloc, u.path.lstrip("/"))
+
+    def _save_snapshot(self, epoch: int) -> None:
+        snapshot = self._snapshot_dict(epoch)
+        path = self.config.snapshot_path
+        if path.startswith("s3://"):
+            self._upload_snapshot(snapshot, path)
+        else:
+            _atomic_save(snapshot, path)
+        print(f"Model snapshot taken and saved at epoch {epoch}")
+
+    def _load_snapshot(self):
+        import fsspec
+
+        try:
+            with fsspec.open(self.config.snapshot_path, "rb") as f:
+                data = torch.load(f, map_location="cpu", weights_only=True)
+        except FileNotFoundError:
+            if self.global_rank == 0:
+                print("Model snapshot not found. Training from scratch.")
+            return
+        snap = ModelSnapshot(**data)
+        self.engine.load_model_state_dict(snap.model_state)
+        self.engine.opt.load_state_dict(snap.optimizer_state)
+        self.last_epoch = snap.final_epoch
+        self.step = snap.step
+        if self.global_rank == 0:
+            print(f"Resuming training from epoch {self.last_epoch + 1}")
+
+    # ------------------------------------------------------------------ loops
+    def _run_batch(self, inputs, labels, train: bool = True) -> torch.Tensor:
+        if train:
+            return self.engine.train_step([(inputs, labels)])
+        with torch.no_grad():
+            _, loss = self.model(self.engine.to_device(inputs), self.engine.to_device(labels))
+        return loss.detach()
+
+    def _run_epoch(self, epoch: int, dataloader: DataLoader, train: bool = True) -> float:
+        if isinstance(dataloader.sampler, DistributedSampler):
+            dataloader.sampler.set_epoch(epoch)
+        self.model.train(train)
+        total, count = None, 0
+        t0 = time.perf_counter()
+        for idx, (x, y) in enumerate(dataloader):
+            if train and self.config.max_steps_per_epoch and idx >= self.config.max_steps_per_epoch:
+                break
+            loss = self._run_batch(x, y, train)
+            total = loss if total is None else total + loss
+            count += 1
+            if train:
+                self.step += 1
+            if idx % self.config.log_every == 0:
+                lg = D.all_reduce_mean(loss.float()).item()
+                if self.global_rank == 0:
+                    dt = time.perf_counter() - t0
+                    tok = x.numel() * self.world * (idx + 1) / max(dt, 1e-9)
+                    gn = self.engine.grad_norm.item() if train else float("nan")
+                    print(f"[GPU{self.global_rank}] Epoch {epoch} | Iter {idx} | "
+                          f"{'Training' if train else 'Test'} loss {lg:.5f} | grad_norm {gn:.3f} | "
+                          f"{tok:,.0f} tok/s", flush=True)
+        if count == 0:
+            return float("nan")
+        mean = D.all_reduce_mean((total / count).float()).item()
+        self.model.train(True)
+        return mean
+
+    def train(self) -> None:
+        start = self.last_epoch + 1
+        for epoch in range(start, self.config.max_epochs):
+            tr = self._run_epoch(epoch, self.train_loader, True)
+            rec = {"epoch": epoch, "train_loss": tr}
+            if self.global_rank == 0 and epoch % self.save_every == 0:
+                self._save_snapshot(epoch)
+            if self.test_loader is not None:
+                rec["test_loss"] = self._run_epoch(epoch, self.test_loader, False)
+            self.history.append(rec)
+            D.barrier()
+
+
+# ====================================================================================== upstream
+class Trainer:
+    """Upstream-minGPT iteration trainer API, on the MI355X step engine."""
+
+    @staticmethod
+    def get_default_config() -> CfgNode:
+        C = CfgNode()
+        C.device = "auto"
+        C.num_workers = 4
+        C.max_iters = None
+        C.batch_size = 64
+        C.learning_rate = 3e-4
+        C.betas = (0.9, 0.95)
+        C.weight_decay = 0.1
+        C.grad_norm_clip = 1.0
+        C.grad_accum_steps = 1
+        return C
+
+    def __init__(self, config, model, train_dataset):
+        self.config = config
+        self.model = model
+        self.train_dataset = train_dataset
+        self.callbacks = defaultdict(list)
+        dev = config.device
+        if dev == "auto":
+            dev = "cuda" if torch.cuda.is_available() else "cpu"
+        if not D.is_initialized():
+            D.init_distributed(device=dev)
+        self.device = dev
+        print("running on device", self.device)
+        decay, _ = param_groups(model)
+        self.engine = StepEngine(model, lr=config.learning_rate, betas=config.betas,
+                                 weight_decay=config.weight_decay, grad_clip=config.grad_norm_clip,
+                                 decay_names=decay,
+                                 device=D.info().device if dev == "cuda" else torch.device("cpu"))
+        self.optimizer = self.engine.opt
+        self.iter_num = 0
+        self.iter_time = 0.0
+        self.iter_dt = 0.0
+        self.loss = None
+
+    def add_callback(self, onevent: str, callback):
+        self.callbacks[onevent].append(callback)
+
+    def set_callback(self, onevent: str, callback):
+        self.callbacks[onevent] = [callback]
+
+    def trigger_callbacks(self, onevent: str):
+        for callback in self.callbacks.get(onevent, []):
+            callback(self)
+
+    def run(self):
+        model, config = self.model, self.config
+        info = D.info()
+        loader = DataLoader(self.train_dataset,
+                            sampler=InfiniteRandomSampler(self.train_dataset, rank=info.rank),
+                            shuffle=False, pin_memory=self.device == "cuda", batch_size=config.batch_size,
+                            num_workers=config.num_workers)
+        model.train()
+        self.iter_num = 0
+        self.iter_time = time.time()
+        data_iter = iter(loader)
+        accum = max(1, getattr(config, "grad_accum_steps", 1))
+        while True:
+            batches = [next(data_iter) for _ in range(accum)]
+            self.loss = self.engine.train_step(batches)
+            self.trigger_callbacks("on_batch_end")
+            self.iter_num += 1
+            tnow = time.time()
+            self.iter_dt = tnow - self.iter_time
+            self.iter_time = tnow
+            if config.max_iters is not None and self.iter_num >= config.max_iters:
+                break

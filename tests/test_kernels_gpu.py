@@ -36,8 +36,11 @@ def test_layernorm_fwd_bwd(M, D):
     yr.backward(dy.float())
     dw = torch.zeros(D, device=DEV)
     db = torch.ones(D, device=DEV)  # accumulates into existing main grad
-    dx = C.layernorm_bwd(dy, x, w, mean, rstd, dw, db)
+    dx = C.layernorm_bwd(dy, x, w, mean, rstd, dw, db, None)
     _close(dx, xr.grad, atol=5e-2)
+    res = _bf(M, D, seed=5)
+    dx2 = C.layernorm_bwd(dy, x, w, mean, rstd, torch.zeros_like(dw), torch.zeros_like(db), res)
+    _close(dx2, xr.grad + res.float(), atol=6e-2)
     torch.testing.assert_close(dw, wr.grad, atol=5e-2 * math.sqrt(M) / 4, rtol=2e-2)
     torch.testing.assert_close(db - 1, br.grad, atol=5e-2 * math.sqrt(M) / 4, rtol=2e-2)
 
