@@ -61,13 +61,11 @@ at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Te
               "layernorm_bwd: shape mismatch");
   DevGuard g(x.device());
   auto dx = at::empty_like(x);
-  auto ws = at::empty({(int64_t)(mg::layernorm_bwd_workspace((int)M, (int)D) / 4)},
-                      x.options().dtype(at::kFloat));
   if (dres.has_value() && dres->defined()) {
     CHECK_BF16(*dres); CHECK_CONTIG(*dres);
     TORCH_CHECK(dres->numel() == x.numel(), "layernorm_bwd: dres shape");
   }
-  mg::layernorm_bwd(bp(dy), bp(x), bp(w), fp(mean), fp(rstd), bp_opt(dres), bp(dx), fp(dw), fp(db), fp(ws),
+  mg::layernorm_bwd(bp(dy), bp(x), bp(w), fp(mean), fp(rstd), bp_opt(dres), bp(dx), fp(dw), fp(db), nullptr,
                     (int)M, (int)D, cur_stream());
   return dx;
 }

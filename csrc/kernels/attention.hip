@@ -64,6 +64,8 @@ struct AttnArgs {
   float dscale;        // 1 / (1 - p)
 };
 
+MG_DEVICE float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }  // v_exp_f32, no denorm fixup
+
 MG_DEVICE bf16x8 lds_row_frag(const char* base, int row, int ch) {
   return *reinterpret_cast<const bf16x8*>(base + lds_off(row, ch));
 }
@@ -115,6 +117,7 @@ MG_DEVICE uint64_t drop_ctr(uint64_t row, int T, int key) {
 }
 
 // =============================================================================== forward
+template <int NKS>  // head-dim tile = 16 * NKS (hd zero-padded up to it)
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[4 * 64 * ROWB];  // K0 V0 K1 V1
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h32 = lane >> 5, l32 = lane & 31;
@@ -136,8 +139,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
     uint4 u = (myq < a.T && d < a.hd) ? ld16(Qg + (long)myq * ld + d) : make_uint4(0, 0, 0, 0);
     qf[ks] = __builtin_bit_cast(bf16x8, u);
   }
-  const int nks = (a.hd + 15) / 16;
-
   f32x16 o0 = {0}, o1 = {0};
   float m = kNegBig, l = 0.f;
   const int kend = min(a.T, q0 + 128);
@@ -166,7 +167,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
         s[sub] = f32x16{0};
-        for (int ks = 0; ks < nks; ++ks)
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks)
           s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
               lds_row_frag(sk, sub * 32 + l32, ks * 2 + h32), qf[ks], s[sub], 0, 0, 0);
       }
@@ -185,14 +187,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
         }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mn = fmaxf(m, mx);
-      const float alpha = exp2f(m - mn);
+      const float alpha = fexp2(m - mn);
       m = mn;
       float rs = 0.f;
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = exp2f(s[sub][r] - mn);
+          const float p = fexp2(s[sub][r] - mn);
           s[sub][r] = p;
           rs += p;
         }
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
           const int r0 = sub * 32 + 16 * st + 4 * h32;
           const int cb = 16 * ((lane >> 4) & 1);
           o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sv, r0, r0 + 8, cb, lane), pf, o0, 0, 0, 0);
-          if (a.hd > 32)
+          if constexpr (NKS > 2)
             o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sv, r0, r0 + 8, 32 + cb, lane), pf, o1, 0, 0, 0);
         }
     }
@@ -284,6 +286,7 @@ constexpr int BWD_LD_OFF = BWD_DQ_OFF + BQ * HD * 4;
 constexpr int BWD_SMEM = BWD_LD_OFF + 2 * BQ * 4;  // 64.5 KiB -> 2 workgroups per CU
 
 // dS^T image per wave: [32 keys][64 q] bf16, 128-B rows, same swizzle (row = key)
+template <int NKS>
 __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h32 = lane >> 5, l32 = lane & 31;
@@ -300,7 +303,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const AttnArgs a) {
   const float* lseg = a.lse + (long)bh * a.T;
   const float* dlg = a.delta + (long)bh * a.T;
   const int mykey = kb0 + 32 * w + l32;
-  const int nks = (a.hd + 15) / 16;
 
   char* sK = smem + BWD_K_OFF;
   char* sdS = smem + BWD_DS_OFF + w * 32 * ROWB;
@@ -379,7 +381,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const AttnArgs a) {
           continue;
         }
         f32x16 s = {0}, dp = {0};
-        for (int ks = 0; ks < nks; ++ks) {
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
           s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_frag(sQ, qs * 32 + l32, ks * 2 + h32), kf[ks], s, 0, 0, 0);
           dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_frag(sdO, qs * 32 + l32, ks * 2 + h32), vf[ks], dp, 0, 0, 0);
         }
@@ -389,7 +392,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const AttnArgs a) {
         for (int r = 0; r < 16; ++r) {
           const int ql = qs * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
           const int q = qbase + ql;
-          float p = exp2f(s[r] * a.scale_log2 - sL[ql]);
+          float p = fexp2(s[r] * a.scale_log2 - sL[ql]);
           if (mykey > q || q >= a.T || mykey >= a.T) p = 0.f;
           float dpv = dp[r];
           float pdrop = p;
@@ -412,7 +415,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const AttnArgs a) {
           const int cb = 16 * ((lane >> 4) & 1);
           dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sdO, r0, r0 + 8, cb, lane), pf, dv0, 0, 0, 0);
           dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sQ, r0, r0 + 8, cb, lane), dsf, dk0, 0, 0, 0);
-          if (a.hd > 32) {
+          if constexpr (NKS > 2) {
             dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sdO, r0, r0 + 8, 32 + cb, lane), pf, dv1, 0, 0, 0);
             dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sQ, r0, r0 + 8, 32 + cb, lane), dsf, dk1, 0, 0, 0);
           }
@@ -437,7 +440,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const AttnArgs a) {
           const int krow = 32 * w + kr0;
           const int cb = 16 * ((lane >> 4) & 1);
           dq0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, lds_tr_frag(sK, krow, krow + 4, cb, lane), dq0, 0, 0, 0);
-          if (a.hd > 32)
+          if constexpr (NKS > 2)
             dq1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, lds_tr_frag(sK, krow, krow + 4, 32 + cb, lane), dq1, 0, 0, 0);
         }
         // dq[q][d]: col = d (lane), rows = q
@@ -445,7 +448,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const AttnArgs a) {
         for (int r = 0; r < 16; ++r) {
           const int ql = qs * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
           atomicAdd(&sdQ[ql * HD + l32], dq0[r]);
-          if (a.hd > 32) atomicAdd(&sdQ[ql * HD + 32 + l32], dq1[r]);
+          if constexpr (NKS > 2) atomicAdd(&sdQ[ql * HD + 32 + l32], dq1[r]);
         }
       }
     }
@@ -543,7 +546,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   mx = block_max<4>(mx, red);
   float sm = 0.f;
   for (int j = threadIdx.x; j < L; j += 256) {
-    const float p = exp2f(sc[j] - mx);
+    const float p = fexp2(sc[j] - mx);
     sc[j] = p;
     sm += p;
   }
@@ -591,7 +594,9 @@ void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, int B, int T, int
   AttnArgs a = make_args(B, T, H, hd, p, seed);
   a.qkv = qkv; a.out = out; a.lse = lse;
   const int grid = cdiv(T, 128) * B * H;
-  attn_fwd_kernel<<<grid, 256, 0, stream>>>(a);
+  if (hd > 32) attn_fwd_kernel<4><<<grid, 256, 0, stream>>>(a);
+  else if (hd > 16) attn_fwd_kernel<2><<<grid, 256, 0, stream>>>(a);
+  else attn_fwd_kernel<1><<<grid, 256, 0, stream>>>(a);
 }
 
 void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse,
@@ -604,7 +609,9 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
   attn_bwd_pre_kernel<<<cdiv(bht, 256), 256, 0, stream>>>(dout, out, delta, B, T, H, hd, H * hd);
   hipMemsetAsync(dq, 0, sizeof(float) * (size_t)B * T * H * hd, stream);
   const int grid = cdiv(T, 128) * B * H;
-  attn_bwd_kernel<<<grid, 256, BWD_SMEM, stream>>>(a);
+  if (hd > 32) attn_bwd_kernel<4><<<grid, 256, BWD_SMEM, stream>>>(a);
+  else if (hd > 16) attn_bwd_kernel<2><<<grid, 256, BWD_SMEM, stream>>>(a);
+  else attn_bwd_kernel<1><<<grid, 256, BWD_SMEM, stream>>>(a);
   const long n8 = (long)B * T * (H * hd / 8);
   attn_dq_finalize_kernel<<<cdiv(n8, 256), 256, 0, stream>>>(dq, dqkv, (long)B * T, H * hd,
                                                              1.f / sqrtf((float)hd));

@@ -56,6 +56,7 @@ struct GemmArgs {
   uint32_t thr;
   float scale;
   int tiles_m, tiles_n;
+  int splits, kchunk;  // split-K (fp32-accumulate layout only): K range per split, multiple of BK
 };
 
 MG_DEVICE int swz_mn(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
@@ -123,10 +124,12 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
   const int wm = wid >> 1, wn = wid & 1;
 
   // XCD-aware bijective remap, then GROUP_M swizzle
-  const int nwg = args.tiles_m * args.tiles_n;
+  const int nblk = args.tiles_m * args.tiles_n * args.splits;
   const int orig = blockIdx.x;
-  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int xcd = orig & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int wgs = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int split = wgs % args.splits;
+  const int wg = wgs / args.splits;
   const int group = GROUP_M * args.tiles_n;
   const int first_m = (wg / group) * GROUP_M;
   const int gm = min(args.tiles_m - first_m, GROUP_M);
@@ -140,10 +143,11 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (args.K + BK - 1) / BK;
+  const int kbeg = split * args.kchunk;
+  const int nk = (min(args.K, kbeg + args.kchunk) - kbeg + BK - 1) / BK;
   uint4 ra[4], rb[4];
-  load_tile<AK>(ra, args.A, args.lda, m0, args.a_ext, 0, args.ka);
-  load_tile<BKC>(rb, args.B, args.ldb, n0, args.b_ext, 0, args.kb);
+  load_tile<AK>(ra, args.A, args.lda, m0, args.a_ext, kbeg, args.ka);
+  load_tile<BKC>(rb, args.B, args.ldb, n0, args.b_ext, kbeg, args.kb);
   store_tile<AK>(smem, ra);
   store_tile<BKC>(smem + TILE_BYTES, rb);
   __syncthreads();
@@ -153,8 +157,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
     const char* sb = sa + TILE_BYTES;
     const bool more = kt + 1 < nk;
     if (more) {
-      load_tile<AK>(ra, args.A, args.lda, m0, args.a_ext, (kt + 1) * BK, args.ka);
-      load_tile<BKC>(rb, args.B, args.ldb, n0, args.b_ext, (kt + 1) * BK, args.kb);
+      load_tile<AK>(ra, args.A, args.lda, m0, args.a_ext, kbeg + (kt + 1) * BK, args.ka);
+      load_tile<BKC>(rb, args.B, args.ldb, n0, args.b_ext, kbeg + (kt + 1) * BK, args.kb);
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -177,6 +181,32 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
     __syncthreads();
   }
 
+  if constexpr (OUTF32) {
+    if (args.splits > 1) {
+      // split-K: fp32 atomics into C.  Stage each wave's 64x64 tile through LDS (row stride 68
+      // floats: conflict-free ds_write_b128) in two 32-row halves, then every atomic
+      // wave-instruction adds 64 contiguous floats of one row (256 B: the full-rate shape).
+      float* ct = reinterpret_cast<float*>(smem) + wid * 32 * 68;
+      float* C = reinterpret_cast<float*>(args.C);
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            *reinterpret_cast<f32x4*>(ct + (ii * 16 + (lane & 15)) * 68 + j * 16 + (lane >> 4) * 4) =
+                acc[half * 2 + ii][j];
+        __syncthreads();
+        const int n = n0 + wn * 64 + lane;
+        for (int r = 0; r < 32; ++r) {
+          const int m = m0 + wm * 64 + half * 32 + r;
+          if (m < args.M && n < args.N) atomicAdd(C + (long)m * args.ldc + n, ct[r * 68 + lane]);
+        }
+        __syncthreads();
+      }
+      return;
+    }
+  }
   // ---- epilogue: lane holds C[m][n..n+3]
   const int nlim = (EPI == 0 && !OUTF32) ? (int)args.ldc : args.N;
 #pragma unroll
@@ -232,7 +262,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmArgs args) {
 
 template <bool AK, bool BKC, int EPI, bool OUTF32>
 void launch(const GemmArgs& a, hipStream_t stream) {
-  const int grid = a.tiles_m * a.tiles_n;
+  const int grid = a.tiles_m * a.tiles_n * a.splits;
   gemm_kernel<AK, BKC, EPI, OUTF32><<<grid, 256, 2 * STAGE_BYTES, stream>>>(a);
 }
 
@@ -252,6 +282,16 @@ void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long l
   a.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   a.tiles_m = cdiv(M, BM);
   a.tiles_n = cdiv(N, BN);
+  a.splits = 1;
+  a.kchunk = cdiv(K, BK) * BK;
+  if (layout == 2) {  // weight gradient: small outputs, huge K -> split K until ~2 blocks per CU
+    const int tiles = a.tiles_m * a.tiles_n;
+    int sp = tiles >= 384 ? 1 : std::min(16, cdiv(512, tiles));
+    const int nkt = cdiv(K, BK);
+    sp = std::min(sp, nkt);
+    a.kchunk = cdiv(nkt, sp) * BK;
+    a.splits = cdiv(K, a.kchunk);
+  }
   if (layout == 0) {
     if (epi == 0) launch<true, true, 0, false>(a, stream);
     else if (epi == 1) launch<true, true, 1, false>(a, stream);

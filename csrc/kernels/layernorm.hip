@@ -7,10 +7,10 @@
 // contiguous bf16 (16-B loads), so the row is read from HBM exactly once and the two-pass
 // (mean, then centred variance) statistics come from registers.  mean/rstd are saved in fp32.
 //
-// Backward: same row mapping.  dx is produced per row; dgamma/dbeta are accumulated per wave in
-// registers over a grid-stride loop, reduced across the block's waves through LDS into a
-// [grid, D] fp32 partial slab, and a second kernel sums the slab deterministically and adds it
-// into the fp32 main-grad buffers (no float atomics, bitwise reproducible).
+// Backward: same row mapping.  dx is produced per row (optionally + the residual-branch gradient);
+// dgamma/dbeta are accumulated per wave in registers over a grid-stride loop, folded across the
+// block's waves through LDS and added into the fp32 main-grad buffers with one atomic per column
+// per block.
 #include "common.h"
 #include "kernels.h"
 
@@ -84,7 +84,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
                                                      const float* __restrict__ rstd,
                                                      const bf16_t* __restrict__ dres,
                                                      bf16_t* __restrict__ dx,
-                                                     float* __restrict__ part, int M, int D) {
+                                                     float* __restrict__ dw,
+                                                     float* __restrict__ db, int M, int D) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float gacc[NV][8], bacc[NV][8], wf[NV][8];
 #pragma unroll
@@ -141,7 +142,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       }
     }
   }
-  // reduce the 4 waves' column partials through LDS, then write this block's partial row.
+  // fold the 4 waves' column partials through LDS, then one fp32 atomic per column per block
+  // straight into the main-grad buffers (64 contiguous floats per wave-instruction: full-rate
+  // atomic shape; 512 blocks x 2D floats is a few MB of atomic traffic).
   extern __shared__ __attribute__((aligned(16))) float red[];  // [4][2*D]
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
@@ -156,22 +159,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
   }
   __syncthreads();
   for (int c = threadIdx.x; c < 2 * D; c += 256) {
-    part[(long)blockIdx.x * 2 * D + c] = red[c] + red[2 * D + c] + red[4 * D + c] + red[6 * D + c];
+    const float v = red[c] + red[2 * D + c] + red[4 * D + c] + red[6 * D + c];
+    if (c < D) atomicAdd(dw + c, v);
+    else atomicAdd(db + c - D, v);
   }
-}
-
-// Sum partial slab [G, 2D] over G; add into dw (first D) and db (second D) main grads.
-__global__ __launch_bounds__(256) void ln_bwd_reduce_kernel(const float* __restrict__ part,
-                                                            float* __restrict__ dw,
-                                                            float* __restrict__ db, int G, int D) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= 2 * D) return;
-  float s = 0.f;
-  for (int g = 0; g < G; ++g) s += part[(long)g * 2 * D + c];
-  if (c < D)
-    dw[c] += s;
-  else
-    db[c - D] += s;
 }
 
 }  // namespace
@@ -200,10 +191,9 @@ void layernorm_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const flo
                    float* workspace, int M, int D, hipStream_t stream) {
   const int grid = ln_bwd_grid(M);
   const size_t smem = sizeof(float) * 8 * D;
-  MG_LN_DISPATCH(ln_bwd_kernel, dy, x, w, mean, rstd, dres, dx, workspace, M, D);
-  ln_bwd_reduce_kernel<<<cdiv(2 * D, 256), 256, 0, stream>>>(workspace, dw, db, grid, D);
+  MG_LN_DISPATCH(ln_bwd_kernel, dy, x, w, mean, rstd, dres, dx, dw, db, M, D);
 }
 
-size_t layernorm_bwd_workspace(int M, int D) { return sizeof(float) * (size_t)ln_bwd_grid(M) * 2 * D; }
+size_t layernorm_bwd_workspace(int M, int D) { return 0; }
 
 }  // namespace mg
