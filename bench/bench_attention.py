@@ -41,9 +41,9 @@ def main():
     dout = torch.randn(B * T, D, device="cuda").to(torch.bfloat16)
     flops_fwd = 4 * B * H * T * T * hd / 2
     for p in (0.0, 0.1):
-        out, lse = C.attention_fwd(qkv, B, T, H, p, 1)
+        out, lse, mask = C.attention_fwd(qkv, B, T, H, p, 1)
         tf = timeit(lambda: C.attention_fwd(qkv, B, T, H, p, 1))
-        tb = timeit(lambda: C.attention_bwd(qkv, out, dout, lse, B, T, H, p, 1))
+        tb = timeit(lambda: C.attention_bwd(qkv, out, dout, lse, mask, B, T, H, p, 1))
         q, k, v = qkv.view(B, T, 3, H, hd).permute(2, 0, 3, 1, 4).unbind(0)
         q, k, v = (t.contiguous().requires_grad_() for t in (q, k, v))
         go = dout.view(B, T, H, hd).transpose(1, 2).contiguous()

@@ -280,14 +280,18 @@ std::vector<at::Tensor> attention_fwd(const at::Tensor& qkv, int64_t B, int64_t 
   DevGuard g(qkv.device());
   auto out = at::empty({B * T, D}, qkv.options());
   auto lse = at::empty({B * H * T}, qkv.options().dtype(at::kFloat));
-  mg::attention_fwd(bp(qkv), bp(out), fp(lse), (int)B, (int)T, (int)H, (int)hd, (float)p,
-                    (uint64_t)seed, cur_stream());
-  return {out, lse};
+  at::Tensor mask = p > 0 ? at::empty({(int64_t)mg::attention_dropout_mask_words((int)B, (int)T, (int)H)},
+                                      qkv.options().dtype(at::kInt))
+                          : at::empty({0}, qkv.options().dtype(at::kInt));
+  mg::attention_fwd(bp(qkv), bp(out), fp(lse),
+                    p > 0 ? reinterpret_cast<uint32_t*>(mask.data_ptr<int>()) : nullptr, (int)B, (int)T,
+                    (int)H, (int)hd, (float)p, (uint64_t)seed, cur_stream());
+  return {out, lse, mask};
 }
 
 at::Tensor attention_bwd(const at::Tensor& qkv, const at::Tensor& out, const at::Tensor& dout,
-                         const at::Tensor& lse, int64_t B, int64_t T, int64_t H, double p,
-                         int64_t seed) {
+                         const at::Tensor& lse, const at::Tensor& mask, int64_t B, int64_t T,
+                         int64_t H, double p, int64_t seed) {
   CHECK_BF16(qkv); CHECK_BF16(out); CHECK_BF16(dout); CHECK_F32(lse);
   CHECK_CONTIG(qkv); CHECK_CONTIG(out); CHECK_CONTIG(dout);
   const int64_t D3 = qkv.size(-1), D = D3 / 3, hd = D / H;
@@ -298,7 +302,15 @@ at::Tensor attention_bwd(const at::Tensor& qkv, const at::Tensor& out, const at:
   auto opts = qkv.options().dtype(at::kFloat);
   auto delta = at::empty({B * H * T}, opts);
   auto dq = at::empty({B * T * D}, opts);
-  mg::attention_bwd(bp(qkv), bp(out), bp(dout), fp(lse), fp(delta), fp(dq), bp(dqkv), (int)B,
+  const uint32_t* mp = nullptr;
+  if (p > 0) {
+    CHECK_DEV(mask);
+    TORCH_CHECK(mask.scalar_type() == at::kInt &&
+                    mask.numel() == (int64_t)mg::attention_dropout_mask_words((int)B, (int)T, (int)H),
+                "attention_bwd: dropout mask from attention_fwd required when p > 0");
+    mp = reinterpret_cast<const uint32_t*>(mask.data_ptr<int>());
+  }
+  mg::attention_bwd(bp(qkv), bp(out), bp(dout), fp(lse), mp, fp(delta), fp(dq), bp(dqkv), (int)B,
                     (int)T, (int)H, (int)hd, (float)p, (uint64_t)seed, cur_stream());
   return dqkv;
 }

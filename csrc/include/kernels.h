@@ -55,12 +55,14 @@ void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long l
           bf16_t* aux, const bf16_t* resid, float p, uint64_t seed, hipStream_t stream);
 
 // attention.hip -- causal flash attention, hd <= 64; qkv [B*T, 3D], out [B*T, D], lse [B*H*T]
-void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, int B, int T, int H, int hd, float p,
-                   uint64_t seed, hipStream_t stream);
+// dmask: dropout keep-bits written by fwd when p > 0 (attention_dropout_mask_words u32), read by bwd
+size_t attention_dropout_mask_words(int B, int T, int H);
+void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, uint32_t* dmask, int B, int T, int H,
+                   int hd, float p, uint64_t seed, hipStream_t stream);
 // delta [B*H*T] and dq [B*T*D] fp32 are workspaces; writes all three slots of dqkv
 void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse,
-                   float* delta, float* dq, bf16_t* dqkv, int B, int T, int H, int hd, float p,
-                   uint64_t seed, hipStream_t stream);
+                   const uint32_t* dmask, float* delta, float* dq, bf16_t* dqkv, int B, int T, int H,
+                   int hd, float p, uint64_t seed, hipStream_t stream);
 
 // one decode step: appends K/V of qkv_new [B, 3D] at row pos of cache [B, Tmax, 3D]; out [B, D]
 void attention_decode(const bf16_t* qkv_new, bf16_t* cache, bf16_t* out, int B, int H, int hd,

@@ -57,11 +57,12 @@ struct AttnArgs {
   const float* delta;  // bwd [B*H*T]
   float* dq;           // bwd [B*T, D] fp32 accumulator
   bf16_t* dqkv;        // bwd [B*T, 3D]
+  uint32_t* dmask;     // dropout keep-bits [B*H*T][2*ceil(T/64)] (fwd writes, bwd reads)
   int B, T, H, hd, D;
   float scale_log2;    // log2(e) / sqrt(hd)
   uint64_t seed;
-  uint32_t thr;
-  float dscale;        // 1 / (1 - p)
+  uint32_t thr;        // 8-bit keep threshold: keep iff random byte >= thr (0 = no dropout)
+  float dscale;        // 1 / (1 - thr/256)
 };
 
 MG_DEVICE float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }  // v_exp_f32, no denorm fixup
@@ -111,11 +112,6 @@ MG_DEVICE void store64(char* lds, const uint4 (&reg)[2]) {
   }
 }
 
-// Philox counter of the attention-dropout mask: row = (b*H + h)*T + q, 4 keys per counter.
-MG_DEVICE uint64_t drop_ctr(uint64_t row, int T, int key) {
-  return row * (uint64_t)((T + 3) >> 2) + (uint64_t)(key >> 2);
-}
-
 // =============================================================================== forward
 template <int NKS>  // head-dim tile = 16 * NKS (hd zero-padded up to it)
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
@@ -145,6 +141,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
   const int ntiles = (kend + 63) / 64;
   const int wave_qmax = q0 + 32 * w + 31;
   const uint64_t drop_row = (uint64_t)bh * a.T + myq;
+  const int ntiles_all = (a.T + 63) / 64;
 
   uint4 rk[2], rv[2];
   load64(rk, Kg, ld, 0, a.T, a.hd);
@@ -203,16 +200,21 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
       o0 *= alpha;
       o1 *= alpha;
       if (a.thr) {  // attention dropout on P (for O only; l uses the undropped P)
+        // one Philox call = 16 random bytes = this lane's 16 elements of a 32-key subtile;
+        // keep iff byte >= thr (8-bit threshold).  The keep bits are stored for the backward.
+        uint32_t bits = 0;
 #pragma unroll
-        for (int sub = 0; sub < 2; ++sub)
+        for (int sub = 0; sub < 2; ++sub) {
+          const uint4 rnd = rand4(a.seed, ((drop_row * (uint64_t)ntiles_all + t) * 2 + h32) * 2 + sub);
+          const uint32_t rr[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int key = k0 + sub * 32 + 8 * g + 4 * h32;
-            const uint4 rnd = rand4(a.seed, drop_ctr(drop_row, a.T, key));
-            const uint32_t rr[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) s[sub][4 * g + j] = rr[j] >= a.thr ? s[sub][4 * g + j] * a.dscale : 0.f;
+          for (int r = 0; r < 16; ++r) {
+            const bool keep = ((rr[r >> 2] >> (8 * (r & 3))) & 0xffu) >= a.thr;
+            s[sub][r] = keep ? s[sub][r] * a.dscale : 0.f;
+            bits |= (uint32_t)keep << (sub * 16 + r);
           }
+        }
+        if (myq < a.T) a.dmask[(long)drop_row * (2 * ntiles_all) + t * 2 + h32] = bits;
       }
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub)
@@ -275,24 +277,23 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restr
 }
 
 constexpr int BQ = 64;  // queries per bwd tile
-// LDS: Q[64 rows], dO[64 rows] (single buffer; next tile prefetched in VGPRs), K[128 rows], dS^T per wave [32 keys][64 q] bf16,
-//      dQ acc [64][64] f32, lse/delta [2][64] f32
+// LDS (single-buffered tiles; the next tile is prefetched in VGPRs while this one computes):
+//   Q [64 q][64 d], dO [64 q][64 d], K block [128 keys][64 d], dS^T image [128 keys][64 q] (bf16),
+//   lse/delta [2][64] f32, dropout keep-words [64 q][4] u32.
 constexpr int BWD_Q_OFF = 0;
 constexpr int BWD_DO_OFF = BWD_Q_OFF + BQ * ROWB;
 constexpr int BWD_K_OFF = BWD_DO_OFF + BQ * ROWB;
 constexpr int BWD_DS_OFF = BWD_K_OFF + 128 * ROWB;
-constexpr int BWD_DQ_OFF = BWD_DS_OFF + 4 * 32 * BQ * 2;
-constexpr int BWD_LD_OFF = BWD_DQ_OFF + BQ * HD * 4;
-constexpr int BWD_SMEM = BWD_LD_OFF + 2 * BQ * 4;  // 64.5 KiB -> 2 workgroups per CU
+constexpr int BWD_LD_OFF = BWD_DS_OFF + 128 * ROWB;
+constexpr int BWD_MW_OFF = BWD_LD_OFF + 2 * BQ * 4;
+constexpr int BWD_SMEM = BWD_MW_OFF + BQ * 4 * 4;  // 49.5 KiB
 
-// dS^T image per wave: [32 keys][64 q] bf16, 128-B rows, same swizzle (row = key)
 template <int NKS>
 __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h32 = lane >> 5, l32 = lane & 31;
-  const int nkb = (a.T + 127) / 128;
+  const int w = threadIdx.x >> 6;
   const int bh = blockIdx.x % (a.B * a.H);
-  const int kb = blockIdx.x / (a.B * a.H);  // light-to-heavy is fine: every block sweeps to T
+  const int kb = blockIdx.x / (a.B * a.H);  // key block 0 (heaviest: sweeps all queries) first
   const int b = bh / a.H, hh = bh % a.H;
   const int kb0 = kb * 128;
   const long ld = 3L * a.D;
@@ -302,54 +303,60 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const AttnArgs a) {
   const bf16_t* dOg = a.dout + (long)b * a.T * a.D + hh * a.hd;
   const float* lseg = a.lse + (long)bh * a.T;
   const float* dlg = a.delta + (long)bh * a.T;
-  const int mykey = kb0 + 32 * w + l32;
-
   char* sK = smem + BWD_K_OFF;
-  char* sdS = smem + BWD_DS_OFF + w * 32 * ROWB;
-  float* sdQ = reinterpret_cast<float*>(smem + BWD_DQ_OFF);
-  float* sLD = reinterpret_cast<float*>(smem + BWD_LD_OFF);
+  char* sdS = smem + BWD_DS_OFF;
+  const float* sL = reinterpret_cast<const float*>(smem + BWD_LD_OFF);
+  const uint32_t* sMW = reinterpret_cast<const uint32_t*>(smem + BWD_MW_OFF);
 
-  // K block -> LDS (for dQ), K/V fragments of this wave's keys -> VGPRs
+  int mykey, wave_kmin;
+  bf16x8 vf[4];  // V^T fragments of this wave's keys stay in VGPRs; K fragments are re-read from sK
   {
+    const int lane = threadIdx.x & 63, h32 = lane >> 5, l32 = lane & 31;
+    mykey = kb0 + 32 * w + l32;
+    wave_kmin = kb0 + 32 * w;
     uint4 r0[2], r1[2];
     load64(r0, Kg, ld, kb0, a.T, a.hd);
     load64(r1, Kg, ld, kb0 + 64, a.T, a.hd);
     store64(sK, r0);
     store64(sK + 64 * ROWB, r1);
-  }
-  bf16x8 kf[4], vf[4];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const int d = ks * 16 + 8 * h32;
-    const bool ok = mykey < a.T && d < a.hd;
-    kf[ks] = __builtin_bit_cast(bf16x8, ok ? ld16(Kg + (long)mykey * ld + d) : make_uint4(0, 0, 0, 0));
-    vf[ks] = __builtin_bit_cast(bf16x8, ok ? ld16(Vg + (long)mykey * ld + d) : make_uint4(0, 0, 0, 0));
+    for (int ks = 0; ks < 4; ++ks) {
+      const int d = ks * 16 + 8 * h32;
+      const bool ok = mykey < a.T && d < a.hd;
+      vf[ks] = __builtin_bit_cast(bf16x8, ok ? ld16(Vg + (long)mykey * ld + d) : make_uint4(0, 0, 0, 0));
+    }
   }
-  for (int i = threadIdx.x; i < BQ * HD; i += 256) sdQ[i] = 0.f;
+  // this lane's dropout bit inside the forward's keep-words (see attn_fwd_kernel)
+  const int mw_col = (w >> 1) * 2 + ((mykey >> 2) & 1);
+  const int mw_bit = ((mykey & 32) >> 1) | (mykey & 3) | (((mykey >> 3) & 3) << 2);
+  const int ntw = 2 * ((a.T + 63) / 64);
+  const int t0w = (kb0 / 64) * 2;
 
   f32x16 dk0 = {0}, dk1 = {0}, dv0 = {0}, dv1 = {0};
   const int qt0 = kb0 / BQ;
   const int nqt = (a.T + BQ - 1) / BQ;
-  const int wave_kmin = kb0 + 32 * w;
 
   uint4 rq[2], rd[2];
-  float rl = 0.f, rdl = 0.f;
+  float rl = 0.f;
+  uint32_t rmw = 0;
   auto issue = [&](int qt) {
     load64(rq, Qg, ld, qt * BQ, a.T, a.hd);
     load64(rd, dOg, a.D, qt * BQ, a.T, a.hd);
-    if (threadIdx.x < BQ) {
-      const int q = qt * BQ + threadIdx.x;
-      rl = q < a.T ? lseg[q] : 0.f;
-      rdl = q < a.T ? dlg[q] : 0.f;
+    const int t = threadIdx.x;
+    if (t < 2 * BQ) {
+      const int q = qt * BQ + (t & (BQ - 1));
+      rl = q < a.T ? (t < BQ ? lseg[q] : dlg[q]) : 0.f;
+    }
+    if (a.thr) {
+      const int q = qt * BQ + (t >> 2), j = t & 3;
+      rmw = (q < a.T && t0w + j < ntw) ? a.dmask[((long)bh * a.T + q) * ntw + t0w + j] : 0u;
     }
   };
   auto commit = [&]() {
     store64(smem + BWD_Q_OFF, rq);
     store64(smem + BWD_DO_OFF, rd);
-    if (threadIdx.x < BQ) {
-      sLD[threadIdx.x] = rl;
-      sLD[BQ + threadIdx.x] = rdl;
-    }
+    if (threadIdx.x < 2 * BQ) reinterpret_cast<float*>(smem + BWD_LD_OFF)[threadIdx.x] = rl;
+    if (a.thr) reinterpret_cast<uint32_t*>(smem + BWD_MW_OFF)[threadIdx.x] = rmw;
   };
   issue(qt0);
   commit();
@@ -358,7 +365,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const AttnArgs a) {
   for (int qt = qt0; qt < nqt; ++qt) {
     const char* sQ = smem + BWD_Q_OFF;
     const char* sdO = smem + BWD_DO_OFF;
-    const float* sL = sLD;
     // opaque per-iteration lane id: keeps the (loop-invariant) LDS addresses from being hoisted
     // into dozens of live VGPRs; they are recomputed with a few VALU ops instead.
     int lane = threadIdx.x & 63;
@@ -367,105 +373,94 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const AttnArgs a) {
     const bool more = qt + 1 < nqt;
     if (more) issue(qt + 1);
     const int qbase = qt * BQ;
-    const bool active = qbase + BQ - 1 >= wave_kmin && wave_kmin < a.T;
-    if (active) {
+    char* myds = sdS + w * 32 * ROWB;  // this wave's 32 key rows of the dS^T image
 #pragma unroll
-      for (int qs = 0; qs < 2; ++qs) {
-        const int qsub0 = qbase + qs * 32;
-        if (qsub0 + 31 < wave_kmin) {  // all queries of this subtile precede every key: P = 0
-          // still must write zeros into the dS^T image for the dQ product
-#pragma unroll
-          for (int g = 0; g < 4; ++g)
-            *reinterpret_cast<uint2*>(sdS + lds_off(l32, (qs * 32 + 8 * g + 4 * h32) >> 3) +
-                                      ((qs * 32 + 8 * g + 4 * h32) & 7) * 2) = make_uint2(0, 0);
-          continue;
-        }
-        f32x16 s = {0}, dp = {0};
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_frag(sQ, qs * 32 + l32, ks * 2 + h32), kf[ks], s, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_frag(sdO, qs * 32 + l32, ks * 2 + h32), vf[ks], dp, 0, 0, 0);
-        }
-        // rows of s/dp = queries qs*32 + (r&3) + 8(r>>2) + 4*h32 ; col = key (lane).
-        // In place: s <- dropped P (for dV), dp <- dS.
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int ql = qs * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
-          const int q = qbase + ql;
-          float p = fexp2(s[r] * a.scale_log2 - sL[ql]);
-          if (mykey > q || q >= a.T || mykey >= a.T) p = 0.f;
-          float dpv = dp[r];
-          float pdrop = p;
-          if (a.thr) {
-            const uint4 rnd = rand4(a.seed, drop_ctr((uint64_t)bh * a.T + q, a.T, mykey));
-            const uint32_t sel = (mykey & 3) == 0 ? rnd.x : (mykey & 3) == 1 ? rnd.y : (mykey & 3) == 2 ? rnd.z : rnd.w;
-            const float z = sel >= a.thr ? a.dscale : 0.f;
-            pdrop = p * z;
-            dpv *= z;
-          }
-          s[r] = pdrop;
-          dp[r] = p * (dpv - sL[BQ + ql]);
-        }
-        // dV^T += dO^T P ; dK^T += Q^T dS   (sum over this subtile's 32 queries)
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const bf16x8 pf = pack_frag(s, st);
-          const bf16x8 dsf = pack_frag(dp, st);
-          const int r0 = qs * 32 + 16 * st + 4 * h32;
-          const int cb = 16 * ((lane >> 4) & 1);
-          dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sdO, r0, r0 + 8, cb, lane), pf, dv0, 0, 0, 0);
-          dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sQ, r0, r0 + 8, cb, lane), dsf, dk0, 0, 0, 0);
-          if constexpr (NKS > 2) {
-            dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sdO, r0, r0 + 8, 32 + cb, lane), pf, dv1, 0, 0, 0);
-            dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sQ, r0, r0 + 8, 32 + cb, lane), dsf, dk1, 0, 0, 0);
-          }
-        }
-        // dS^T image [key = lane][q]: 4 consecutive q per 8-byte write
+    for (int qs = 0; qs < 2; ++qs) {
+      const int qsub0 = qbase + qs * 32;
+      if (qsub0 + 31 < wave_kmin || wave_kmin >= a.T) {  // every query precedes every key: dS = 0
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int qc = qs * 32 + 8 * g + 4 * h32;
-          *reinterpret_cast<uint2*>(sdS + lds_off(l32, qc >> 3) + (qc & 7) * 2) =
-              make_uint2(pack2(dp[4 * g], dp[4 * g + 1]), pack2(dp[4 * g + 2], dp[4 * g + 3]));
+          *reinterpret_cast<uint2*>(myds + lds_off(l32, qc >> 3) + (qc & 7) * 2) = make_uint2(0, 0);
+        }
+        continue;
+      }
+      f32x16 s = {0}, dp = {0};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_frag(sQ, qs * 32 + l32, ks * 2 + h32),
+                                                    lds_row_frag(sK, 32 * w + l32, ks * 2 + h32), s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_frag(sdO, qs * 32 + l32, ks * 2 + h32), vf[ks], dp, 0, 0, 0);
+      }
+      // rows = queries qs*32 + (r&3) + 8(r>>2) + 4*h32 ; col = key (lane).  In place:
+      // s <- dropped P (dV operand), dp <- dS = P * (dP~ * Z - delta).
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ql = qs * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+        const int q = qbase + ql;
+        float p = fexp2(s[r] * a.scale_log2 - sL[ql]);
+        if (mykey > q || q >= a.T) p = 0.f;
+        float dpv = dp[r], pdrop = p;
+        if (a.thr) {
+          const float z = (sMW[ql * 4 + mw_col] >> mw_bit) & 1u ? a.dscale : 0.f;
+          pdrop = p * z;
+          dpv *= z;
+        }
+        s[r] = pdrop;
+        dp[r] = p * (dpv - sL[BQ + ql]);
+      }
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const bf16x8 pf = pack_frag(s, st);
+        const bf16x8 dsf = pack_frag(dp, st);
+        const int r0 = qs * 32 + 16 * st + 4 * h32;
+        const int cb = 16 * ((lane >> 4) & 1);
+        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sdO, r0, r0 + 8, cb, lane), pf, dv0, 0, 0, 0);
+        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sQ, r0, r0 + 8, cb, lane), dsf, dk0, 0, 0, 0);
+        if constexpr (NKS > 2) {
+          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sdO, r0, r0 + 8, 32 + cb, lane), pf, dv1, 0, 0, 0);
+          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sQ, r0, r0 + 8, 32 + cb, lane), dsf, dk1, 0, 0, 0);
         }
       }
-      // dQ partial = dS K over this wave's 32 keys: A = dS [q x key] (tr-read of dS^T image),
-      // B = K [key x d] (tr-read of the K block image); natural k order on both sides.
 #pragma unroll
-      for (int qs = 0; qs < 2; ++qs) {
-        f32x16 dq0 = {0}, dq1 = {0};
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {  // 32 keys = 2 k-steps of 16
-          const int kr0 = kk * 16 + 8 * h32;
-          const bf16x8 af = lds_tr_frag(sdS, kr0, kr0 + 4, qs * 32 + 16 * ((lane >> 4) & 1), lane);
-          const int krow = 32 * w + kr0;
-          const int cb = 16 * ((lane >> 4) & 1);
-          dq0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, lds_tr_frag(sK, krow, krow + 4, cb, lane), dq0, 0, 0, 0);
-          if constexpr (NKS > 2)
-            dq1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, lds_tr_frag(sK, krow, krow + 4, 32 + cb, lane), dq1, 0, 0, 0);
-        }
-        // dq[q][d]: col = d (lane), rows = q
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int ql = qs * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
-          atomicAdd(&sdQ[ql * HD + l32], dq0[r]);
-          if constexpr (NKS > 2) atomicAdd(&sdQ[ql * HD + 32 + l32], dq1[r]);
-        }
+      for (int g = 0; g < 4; ++g) {  // dS^T image row = key, 4 consecutive q per 8-byte write
+        const int qc = qs * 32 + 8 * g + 4 * h32;
+        *reinterpret_cast<uint2*>(myds + lds_off(l32, qc >> 3) + (qc & 7) * 2) =
+            make_uint2(pack2(dp[4 * g], dp[4 * g + 1]), pack2(dp[4 * g + 2], dp[4 * g + 3]));
       }
     }
-    __syncthreads();  // every wave is done with the Q/dO tile and has added its dQ partial
-    // flush the summed dQ tile to global (fp32 atomics, 64 contiguous floats per wave-instruction)
-    for (int i = threadIdx.x; i < BQ * HD; i += 256) {
-      const int ql = i / HD, d = i % HD;
-      const int q = qbase + ql;
-      const float v = sdQ[i];
-      sdQ[i] = 0.f;
-      if (q < a.T && d < a.hd && v != 0.f) atomicAdd(a.dq + ((long)b * a.T + q) * a.D + hh * a.hd + d, v);
+    __syncthreads();  // dS of all 128 keys in LDS; Q/dO tile no longer needed
+    // dQ[64 q][64 d] = dS[64 q][128 keys] K[128 keys][64 d]: wave w owns the 32x32 output tile
+    // (qs = w>>1, dblk = w&1) over all 128 keys -- no cross-wave reduction, one fp32 atomic per
+    // element per workgroup (two 128-B row segments per wave-instruction).
+    {
+      const int qs = w >> 1, dblk = w & 1;
+      if (dblk * 32 < a.hd && qbase + qs * 32 + 31 >= kb0) {
+        f32x16 dq = {0};
+        const int cb = 16 * ((lane >> 4) & 1);
+#pragma unroll 2
+        for (int kk = 0; kk < 8; ++kk) {
+          const int kr0 = kk * 16 + 8 * h32;
+          const bf16x8 af = lds_tr_frag(sdS, kr0, kr0 + 4, qs * 32 + cb, lane);
+          dq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, lds_tr_frag(sK, kr0, kr0 + 4, dblk * 32 + cb, lane), dq, 0, 0, 0);
+        }
+        const int d = dblk * 32 + l32;
+        if (d < a.hd) {
+          float* dqb = a.dq + ((long)b * a.T) * a.D + hh * a.hd + d;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int q = qbase + qs * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+            if (q < a.T) atomicAdd(dqb + (long)q * a.D, dq[r]);
+          }
+        }
+      }
     }
     if (more) commit();
     __syncthreads();
   }
 
   // dK (scaled), dV -> dqkv K / V slots ; lane holds d = (r&3) + 8(r>>2) + 4*h32 (+32), key = lane
+  const int lane = threadIdx.x & 63, h32 = lane >> 5;
   if (mykey < a.T) {
     const float sc = a.scale_log2 * 0.6931471805599453f;  // 1/sqrt(hd)
     bf16_t* krow = a.dqkv + ((long)b * a.T + mykey) * ld + a.D + hh * a.hd;
@@ -584,15 +579,23 @@ static AttnArgs make_args(int B, int T, int H, int hd, float p, uint64_t seed) {
   a.B = B; a.T = T; a.H = H; a.hd = hd; a.D = H * hd;
   a.scale_log2 = 1.4426950408889634f / sqrtf((float)hd);
   a.seed = seed;
-  a.thr = p > 0.f ? dropout_threshold(p) : 0u;
-  a.dscale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  // 8-bit dropout threshold (as FlashAttention does): effective p = thr / 256
+  int thr = p > 0.f ? (int)lrintf(p * 256.f) : 0;
+  if (p > 0.f) thr = thr < 1 ? 1 : (thr > 255 ? 255 : thr);
+  a.thr = (uint32_t)thr;
+  a.dscale = thr ? 256.f / (256.f - (float)thr) : 1.f;
   return a;
 }
 
-void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, int B, int T, int H, int hd, float p,
-                   uint64_t seed, hipStream_t stream) {
+size_t attention_dropout_mask_words(int B, int T, int H) {
+  return (size_t)B * H * T * 2 * ((T + 63) / 64);
+}
+
+void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, uint32_t* dmask, int B, int T, int H,
+                   int hd, float p, uint64_t seed, hipStream_t stream) {
   AttnArgs a = make_args(B, T, H, hd, p, seed);
-  a.qkv = qkv; a.out = out; a.lse = lse;
+  a.qkv = qkv; a.out = out; a.lse = lse; a.dmask = dmask;
+  if (a.thr && !dmask) a.thr = 0;
   const int grid = cdiv(T, 128) * B * H;
   if (hd > 32) attn_fwd_kernel<4><<<grid, 256, 0, stream>>>(a);
   else if (hd > 16) attn_fwd_kernel<2><<<grid, 256, 0, stream>>>(a);
@@ -600,11 +603,12 @@ void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, int B, int T, int
 }
 
 void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse,
-                   float* delta, float* dq, bf16_t* dqkv, int B, int T, int H, int hd, float p,
-                   uint64_t seed, hipStream_t stream) {
+                   const uint32_t* dmask, float* delta, float* dq, bf16_t* dqkv, int B, int T, int H,
+                   int hd, float p, uint64_t seed, hipStream_t stream) {
   AttnArgs a = make_args(B, T, H, hd, p, seed);
   a.qkv = qkv; a.out = dqkv; a.lse = const_cast<float*>(lse); a.dout = dout; a.delta = delta;
-  a.dq = dq; a.dqkv = dqkv;
+  a.dq = dq; a.dqkv = dqkv; a.dmask = const_cast<uint32_t*>(dmask);
+  if (a.thr && !dmask) a.thr = 0;
   const long bht = (long)B * H * T;
   attn_bwd_pre_kernel<<<cdiv(bht, 256), 256, 0, stream>>>(dout, out, delta, B, T, H, hd, H * hd);
   hipMemsetAsync(dq, 0, sizeof(float) * (size_t)B * T * H * hd, stream);

@@ -117,7 +117,7 @@ class _GpuCache:
             qkv = G.gemm_nt(h, bf(a.c_attn.weight), bias=bf(a.c_attn.bias), epi="bias")
             if pos0 == 0:
                 self.caches[i][:, :T].copy_(qkv.view(B, T, 3 * D))
-                y, _ = C.attention_fwd(qkv, B, T, H, 0.0, 0)
+                y, _, _ = C.attention_fwd(qkv, B, T, H, 0.0, 0)
             else:
                 y = C.attention_decode(qkv, self.caches[i], H, pos0)
             x = G.gemm_nt(y, bf(a.c_proj.weight), bias=bf(a.c_proj.bias), epi="resid", resid=x)

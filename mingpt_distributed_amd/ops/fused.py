@@ -64,13 +64,13 @@ class TransformerBlockFn(torch.autograd.Function):
                  new_seed() if p_resid > 0 else 0)
         h, mean1, rstd1 = C.layernorm_fwd(x, ln1w, ln1b, eps)
         qkv = G.gemm_nt(h, wqkv, bias=bqkv, epi="bias")
-        y, lse = C.attention_fwd(qkv, B, T, H, float(p_attn), seeds[0])
+        y, lse, amask = C.attention_fwd(qkv, B, T, H, float(p_attn), seeds[0])
         x1 = G.gemm_nt(y, wo, bias=bo, epi="resid", resid=x, p=p_resid, seed=seeds[1])
         h2, mean2, rstd2 = C.layernorm_fwd(x1, ln2w, ln2b, eps)
         pre = torch.empty((x.shape[0], wfc.shape[0]), dtype=torch.bfloat16, device=x.device)
         u = G.gemm_nt(h2, wfc, bias=bfc, epi="gelu", pre_out=pre)
         x2 = G.gemm_nt(u, wp, bias=bp, epi="resid", resid=x1, p=p_resid, seed=seeds[2])
-        ctx.save_for_backward(x, h, mean1, rstd1, qkv, y, lse, x1, h2, mean2, rstd2, pre, u)
+        ctx.save_for_backward(x, h, mean1, rstd1, qkv, y, lse, amask, x1, h2, mean2, rstd2, pre, u)
         ctx.params = (ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, wfc, bfc, wp, bp)
         ctx.cfg, ctx.seeds = cfg, seeds
         for prm in ctx.params:
@@ -81,7 +81,7 @@ class TransformerBlockFn(torch.autograd.Function):
     def backward(ctx, dx2):
         B, T, H, p_attn, p_resid, eps = ctx.cfg
         C = ext()
-        x, h, mean1, rstd1, qkv, y, lse, x1, h2, mean2, rstd2, pre, u = ctx.saved_tensors
+        x, h, mean1, rstd1, qkv, y, lse, amask, x1, h2, mean2, rstd2, pre, u = ctx.saved_tensors
         ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, wfc, bfc, wp, bp = ctx.params
         dx2 = dx2.contiguous()
         g = {}
@@ -101,7 +101,7 @@ class TransformerBlockFn(torch.autograd.Function):
         G.gemm_tn_acc(dz, y, g[id(wo)][0])
         C.bias_grad(dz, g[id(bo)][0])
         dy = G.gemm_nn(dz, wo)
-        dqkv = C.attention_bwd(qkv, y, dy, lse, B, T, H, float(p_attn), ctx.seeds[0])
+        dqkv = C.attention_bwd(qkv, y, dy, lse, amask, B, T, H, float(p_attn), ctx.seeds[0])
         G.gemm_tn_acc(dqkv, h, g[id(wqkv)][0])
         C.bias_grad(dqkv, g[id(bqkv)][0])
         dh = G.gemm_nn(dqkv, wqkv)

@@ -23,7 +23,7 @@ def test_attention_fwd_bwd(B, T, H, hd):
     torch.manual_seed(0)
     D = H * hd
     qkv = torch.randn(B * T, 3 * D, device=DEV).to(torch.bfloat16)
-    out, lse = C.attention_fwd(qkv, B, T, H, 0.0, 0)
+    out, lse, mask = C.attention_fwd(qkv, B, T, H, 0.0, 0)
     qkv_r = qkv.float().requires_grad_()
     q, k, v = _split(qkv_r, B, T, H)
     ref = R.causal_attention(q, k, v, 0.0, False).transpose(1, 2).reshape(B * T, D)
@@ -35,7 +35,7 @@ def test_attention_fwd_bwd(B, T, H, hd):
     torch.testing.assert_close(lse.view(B, H, T), lse_ref.detach(), atol=2e-2, rtol=1e-3)
     dout = torch.randn(B * T, D, device=DEV).to(torch.bfloat16)
     ref.backward(dout.float())
-    dqkv = C.attention_bwd(qkv, out, dout, lse, B, T, H, 0.0, 0)
+    dqkv = C.attention_bwd(qkv, out, dout, lse, mask, B, T, H, 0.0, 0)
     g = qkv_r.grad
     scale = g.abs().max().item()
     torch.testing.assert_close(dqkv.float(), g, atol=3e-2 * max(1.0, scale / 4), rtol=5e-2)
@@ -46,10 +46,10 @@ def test_attention_causality():
     C = ext()
     B, T, H, hd = 1, 256, 2, 64
     qkv = torch.randn(B * T, 3 * H * hd, device=DEV).to(torch.bfloat16)
-    out1, _ = C.attention_fwd(qkv, B, T, H, 0.0, 0)
+    out1 = C.attention_fwd(qkv, B, T, H, 0.0, 0)[0]
     qkv2 = qkv.clone()
     qkv2[200:] += 1.0
-    out2, _ = C.attention_fwd(qkv2, B, T, H, 0.0, 0)
+    out2 = C.attention_fwd(qkv2, B, T, H, 0.0, 0)[0]
     assert torch.equal(out1[:200], out2[:200])
     assert not torch.equal(out1[200:], out2[200:])
 
@@ -58,15 +58,15 @@ def test_attention_dropout_deterministic():
     C = ext()
     B, T, H, hd = 2, 256, 2, 64
     qkv = torch.randn(B * T, 3 * H * hd, device=DEV).to(torch.bfloat16)
-    o1, l1 = C.attention_fwd(qkv, B, T, H, 0.1, 42)
-    o2, _ = C.attention_fwd(qkv, B, T, H, 0.1, 42)
-    o3, _ = C.attention_fwd(qkv, B, T, H, 0.1, 43)
-    o0, l0 = C.attention_fwd(qkv, B, T, H, 0.0, 0)
+    o1, l1, m1 = C.attention_fwd(qkv, B, T, H, 0.1, 42)
+    o2, _, m2 = C.attention_fwd(qkv, B, T, H, 0.1, 42)
+    o3, _, _ = C.attention_fwd(qkv, B, T, H, 0.1, 43)
+    o0, l0, _ = C.attention_fwd(qkv, B, T, H, 0.0, 0)
     assert torch.equal(o1, o2) and not torch.equal(o1, o3)
     torch.testing.assert_close(l1, l0)  # softmax statistics use the undropped P
     dout = torch.randn_like(o1)
-    d1 = C.attention_bwd(qkv, o1, dout, l1, B, T, H, 0.1, 42)
-    d2 = C.attention_bwd(qkv, o1, dout, l1, B, T, H, 0.1, 42)
+    d1 = C.attention_bwd(qkv, o1, dout, l1, m1, B, T, H, 0.1, 42)
+    d2 = C.attention_bwd(qkv, o1, dout, l1, m2, B, T, H, 0.1, 42)
     D = H * hd  # dK/dV are register-accumulated: bitwise reproducible; dQ uses fp32 atomics
     assert torch.equal(d1[:, D:], d2[:, D:]) and torch.isfinite(d1.float()).all()
     torch.testing.assert_close(d1[:, :D].float(), d2[:, :D].float(), atol=1e-2, rtol=1e-2)
@@ -79,8 +79,8 @@ def test_attention_dropout_gradient_directional():
     torch.manual_seed(1)
     qkv = (torch.randn(B * T, 3 * H * hd, device=DEV) * 0.5).to(torch.bfloat16)
     w = torch.randn(B * T, H * hd, device=DEV)
-    o, lse = C.attention_fwd(qkv, B, T, H, 0.2, 7)
-    d = C.attention_bwd(qkv, o, w.to(torch.bfloat16), lse, B, T, H, 0.2, 7).float()
+    o, lse, msk = C.attention_fwd(qkv, B, T, H, 0.2, 7)
+    d = C.attention_bwd(qkv, o, w.to(torch.bfloat16), lse, msk, B, T, H, 0.2, 7).float()
     delta = torch.randn_like(qkv.float())
     eps = 0.05
     fp = (C.attention_fwd((qkv.float() + eps * delta).to(torch.bfloat16), B, T, H, 0.2, 7)[0].float() * w).sum()
@@ -88,3 +88,40 @@ def test_attention_dropout_gradient_directional():
     fd = (fp - fm) / (2 * eps)
     an = (d * delta).sum()
     assert abs(fd.item() - an.item()) < 0.08 * abs(an.item()) + 1.0
+
+
+def _dense_keep(mask, B, T, H):
+    """Dense [B, H, T, T] keep matrix from the forward's keep-bit words (layout: attention.hip)."""
+    ntiles = (T + 63) // 64
+    words = mask.view(B * H * T, ntiles * 2).to(torch.int64) & 0xFFFFFFFF
+    key = torch.arange(T, device=mask.device)
+    t, kk = key // 64, key % 64
+    col = t * 2 + ((kk >> 2) & 1)
+    bit = ((kk & 32) >> 1) | (kk & 3) | (((kk >> 3) & 3) << 2)
+    w = words[:, col]  # [BHT, T]
+    return ((w >> bit) & 1).view(B, H, T, T).float()
+
+
+@pytest.mark.parametrize("T", [128, 320])
+def test_attention_dropout_exact(T):
+    """Forward and backward with dropout vs an fp32 reference that uses the kernel's exact mask."""
+    C = ext()
+    B, H, hd, p = 2, 2, 64, 0.1
+    torch.manual_seed(3)
+    D = H * hd
+    qkv = torch.randn(B * T, 3 * D, device=DEV).to(torch.bfloat16)
+    out, lse, mask = C.attention_fwd(qkv, B, T, H, p, 11)
+    thr = round(p * 256)
+    keep = _dense_keep(mask, B, T, H) * (256.0 / (256 - thr))
+    qkv_r = qkv.float().requires_grad_()
+    q, k, v = _split(qkv_r, B, T, H)
+    att = (q @ k.transpose(-1, -2)) / hd ** 0.5
+    att = att.masked_fill(~torch.ones(T, T, dtype=torch.bool, device=DEV).tril(), float("-inf")).softmax(-1)
+    ref = ((att * keep) @ v).transpose(1, 2).reshape(B * T, D)
+    torch.testing.assert_close(out.float(), ref.detach(), atol=3e-2, rtol=3e-2)
+    dout = torch.randn(B * T, D, device=DEV).to(torch.bfloat16)
+    ref.backward(dout.float())
+    dqkv = C.attention_bwd(qkv, out, dout, lse, mask, B, T, H, p, 11)
+    g = qkv_r.grad
+    scale = g.abs().max().item()
+    torch.testing.assert_close(dqkv.float(), g, atol=3e-2 * max(1.0, scale / 4), rtol=5e-2)
