@@ -254,17 +254,18 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
 }
 
 // =============================================================================== backward
-// delta[bh*T + t] = sum_d dO * O ; also zero dq
+// delta[(b*H + h)*T + t] = sum_d dO * O.  Thread i covers (b, t, h) with h fastest, so a wave
+// reads contiguous 128-B head rows of consecutive heads (coalesced), not rows D*2 bytes apart.
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restrict__ dout,
                                                            const bf16_t* __restrict__ out,
                                                            float* __restrict__ delta, int B, int T,
                                                            int H, int hd, int D) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;  // over B*H*T
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;  // over B*T*H
   if (i >= (long)B * H * T) return;
-  const int t = (int)(i % T);
-  const long bh = i / T;
-  const int b = (int)(bh / H), hh = (int)(bh % H);
-  const long off = ((long)b * T + t) * D + hh * hd;
+  const int hh = (int)(i % H);
+  const long bt = i / H;
+  const int t = (int)(bt % T), b = (int)(bt / T);
+  const long off = bt * D + hh * hd;
   float s = 0.f;
   for (int d = 0; d < hd; d += 8) {
     float x[8], y[8];
@@ -273,7 +274,7 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restr
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += x[j] * y[j];
   }
-  delta[i] = s;
+  delta[((long)b * H + hh) * T + t] = s;
 }
 
 constexpr int BQ = 64;  // queries per bwd tile

@@ -128,6 +128,7 @@ class HeadLossFn(torch.autograd.Function):
         for prm in ctx.params:
             note_use(prm)
         ctx.mark_non_differentiable(logits)
+        ctx.set_materialize_grads(False)  # never build a [M, Vpad] zero grad for the logits
         return logits, out[0]
 
     @staticmethod

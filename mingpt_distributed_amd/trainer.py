@@ -40,6 +40,12 @@ from .utils.config import CfgNode
 
 
 # ====================================================================================== engine
+def _fold_grad(p):
+    if p.grad is not None:
+        p.main_grad.add_(p.grad.to(p.main_grad.dtype))
+        p.grad = None
+
+
 class StepEngine:
     def __init__(self, model: torch.nn.Module, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
                  weight_decay: float = 0.1, grad_clip: float = 1.0, decay_names=None,
@@ -62,6 +68,12 @@ class StepEngine:
         self.dp = DataParallelEngine(self.store, bucket_mb=bucket_mb, reduce_dtype=reduce_dtype) \
             if D.is_initialized() and torch.distributed.get_world_size() > 1 else None
         self.world = self.dp.world if self.dp else 1
+        self._hooks = []
+        if self.dp is None:
+            # single process: ops that return ordinary autograd grads (the CPU reference path)
+            # are folded into the fp32 main-grad buffer the optimizer reads
+            for p in self.store.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(_fold_grad))
 
     @classmethod
     def from_torch_optimizer(cls, model, optimizer: torch.optim.Optimizer, grad_clip: float, **kw):
