@@ -38,24 +38,35 @@ def main():
     Vp = (V + 127) // 128 * 128
     r = lambda *s: torch.randn(*s, device="cuda").to(torch.bfloat16)
     rows = []
+    C = __import__("mingpt_distributed_amd.ops._ext", fromlist=["ext"]).ext()
+
+    def both(fn):  # A/B the tile configs of the hand-written kernel in one process (auto, 128, 256, 256x128)
+        out = []
+        for v in (0, 1, 2, 3):
+            C.gemm_set_variant(v)
+            out.append(timeit(fn))
+        C.gemm_set_variant(0)
+        return out[0], out
+
+    variants = {}
     for name, N, K in [("qkv", 3 * D, D), ("attn_proj", D, D), ("fc", 4 * D, D), ("mlp_proj", D, 4 * D),
                        ("lm_head", V, D)]:
         x, w = r(M, K), r(N, K)
         ld = Vp if name == "lm_head" else None
-        t_mine = timeit(lambda: G.gemm_nt(x, w, ld=ld))
+        t_mine, variants[("fwd", name)] = both(lambda: G.gemm_nt(x, w, ld=ld))
         t_blas = timeit(lambda: torch.mm(x, w.t()))
         rows.append(("fwd_nt", name, M, N, K, t_mine, t_blas))
         # dgrad: dx[M,K] = dy[M,N] @ w[N,K]
         dy = r(M, Vp if name == "lm_head" else N)
         if name == "lm_head":
             dy[:, V:] = 0
-        t_mine = timeit(lambda: G.gemm_nn(dy, w))
+        t_mine, variants[("dgrad", name)] = both(lambda: G.gemm_nn(dy, w))
         dyv = dy[:, :N] if name == "lm_head" else dy
         t_blas = timeit(lambda: torch.mm(dyv, w))
         rows.append(("dgrad_nn", name, M, K, N, t_mine, t_blas))
         # wgrad: dw[N,K] += dy^T x
         c = torch.zeros(N, K, device="cuda")
-        t_mine = timeit(lambda: G.gemm_tn_acc(dy, x, c, n_valid=N))
+        t_mine, variants[("wgrad", name)] = both(lambda: G.gemm_tn_acc(dy, x, c, n_valid=N))
         t_blas = timeit(lambda: torch.mm(dyv.t(), x))
         rows.append(("wgrad_tn", name, N, K, M, t_mine, t_blas))
     tot_m = tot_b = 0.0
@@ -68,6 +79,14 @@ def main():
                           "hipblaslt_tflops": round(fl / tb / 1e9, 1), "speedup": round(tb / tm, 3)}),
               flush=True)
     print(json.dumps({"total_mine_ms": round(tot_m, 3), "total_hipblaslt_ms": round(tot_b, 3)}))
+    print(json.dumps({"variant_ms(auto,t128,t256,t256x128)": {f"{k[0]}:{k[1]}": [round(t, 4) for t in v] for k, v in variants.items()}}))
+    n = 4096
+    a4, b4 = r(n, n), r(n, n)
+    t4, v4 = both(lambda: G.gemm_nt(a4, b4))
+    tb4 = timeit(lambda: torch.mm(a4, b4.t()))
+    print(json.dumps({"gemm_4096^3_tflops": {k: round(2 * n ** 3 / t / 1e9, 1) for k, t in
+                                              zip(("auto", "t128", "t256", "t256x128"), v4)} |
+                      {"hipblaslt": round(2 * n ** 3 / tb4 / 1e9, 1)}}))
 
 
 if __name__ == "__main__":

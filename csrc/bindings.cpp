@@ -264,10 +264,12 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     TORCH_CHECK(resid->numel() == c.numel() && ldc == N, "gemm: resid shape");
     res_p = bp(*resid);
   }
+  TORCH_CHECK((size_t)a.numel() * 2 < 0xFFFFFF00u && (size_t)b.numel() * 2 < 0xFFFFFF00u,
+              "gemm: operands must be < 4 GiB (32-bit buffer offsets)");
   DevGuard g(a.device());
   mg::gemm((int)layout, (int)epi, bp(a), bp(b), c.data_ptr(), lda, ldb, ldc, (int)M, (int)N, (int)K,
            (int)a_ext, (int)b_ext, (int)ka, (int)kb, bias_p, aux_p, res_p, (float)p, (uint64_t)seed,
-           cur_stream());
+           cur_stream(), (size_t)a.numel() * 2, (size_t)b.numel() * 2);
 }
 
 // ------------------------------------------------------------------------------- attention
@@ -348,6 +350,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dropout_bwd", &dropout_bwd);
   m.def("bias_grad", &bias_grad);
   m.def("gemm", &gemm);
+  m.def("gemm_set_variant", &mg::gemm_set_variant);
+  m.def("gemm_get_variant", &mg::gemm_get_variant);
   m.def("attention_fwd", &attention_fwd);
   m.def("attention_bwd", &attention_bwd);
   m.def("attention_decode", &attention_decode);

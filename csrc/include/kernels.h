@@ -52,7 +52,10 @@ void bias_grad(const bf16_t* dy, float* db, long M, int N, hipStream_t stream);
 // epi: 0 none, 1 bias, 2 bias+gelu (pre -> aux), 3 resid + dropout(acc + bias), 4 acc*gelu'(aux)
 void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long lda, long ldb,
           long ldc, int M, int N, int K, int a_ext, int b_ext, int ka, int kb, const bf16_t* bias,
-          bf16_t* aux, const bf16_t* resid, float p, uint64_t seed, hipStream_t stream);
+          bf16_t* aux, const bf16_t* resid, float p, uint64_t seed, hipStream_t stream,
+          size_t a_bytes, size_t b_bytes);  // operand sizes in bytes (< 4 GiB for the DMA path)
+void gemm_set_variant(int v);  // 0 register staging, 1 LDS-DMA staging (default)
+int gemm_get_variant();
 
 // attention.hip -- causal flash attention, hd <= 64; qkv [B*T, 3D], out [B*T, D], lse [B*H*T]
 // dmask: dropout keep-bits written by fwd when p > 0 (attention_dropout_mask_words u32), read by bwd

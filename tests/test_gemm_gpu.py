@@ -9,6 +9,16 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+@pytest.fixture(autouse=True, params=[0, 1, 2, 3], ids=["auto", "t128", "t256", "t256x128"])
+def tile_config(request):
+    """Run every GEMM test under each tile configuration of gemm.hip (0 = per-shape choice)."""
+    from mingpt_distributed_amd.ops._ext import ext
+
+    ext().gemm_set_variant(request.param)
+    yield request.param
+    ext().gemm_set_variant(0)
+
+
 def _bf(*shape, seed=0, scale=1.0):
     g = torch.Generator(device="cpu").manual_seed(seed)
     return (torch.randn(*shape, generator=g) * scale).to(DEV, torch.bfloat16)
