@@ -206,6 +206,17 @@ at::Tensor dropout_bwd(const at::Tensor& dy, double p, int64_t seed) {
   return dx;
 }
 
+// dx = dropout_bwd(dy) and db += colsum(dx) in one pass
+at::Tensor dropout_bias_grad(const at::Tensor& dy, const at::Tensor& db, double p, int64_t seed) {
+  CHECK_BF16(dy); CHECK_F32(db); CHECK_CONTIG(dy);
+  const int64_t N = dy.size(-1), M = dy.numel() / N;
+  TORCH_CHECK(N % 8 == 0 && db.numel() == N, "dropout_bias_grad: shape mismatch");
+  DevGuard g(dy.device());
+  auto dx = at::empty_like(dy);
+  mg::dropout_bias_grad(bp(dy), bp(dx), fp(db), M, (int)N, (float)p, (uint64_t)seed, cur_stream());
+  return dx;
+}
+
 void bias_grad(const at::Tensor& dy, const at::Tensor& db) {
   CHECK_BF16(dy); CHECK_F32(db); CHECK_CONTIG(dy);
   const int64_t N = dy.size(-1), M = dy.numel() / N;
@@ -299,6 +310,7 @@ at::Tensor attention_bwd(const at::Tensor& qkv, const at::Tensor& out, const at:
   const int64_t D3 = qkv.size(-1), D = D3 / 3, hd = D / H;
   TORCH_CHECK(qkv.numel() == B * T * D3 && out.numel() == B * T * D && dout.numel() == B * T * D &&
               lse.numel() == B * H * T && hd % 8 == 0 && hd <= 64, "attention_bwd: shape mismatch");
+  TORCH_CHECK((hd & (hd - 1)) == 0, "attention_bwd: head dim must be a power of two (8..64)");
   DevGuard g(qkv.device());
   auto dqkv = at::empty_like(qkv);
   auto opts = qkv.options().dtype(at::kFloat);
@@ -349,6 +361,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_bwd", &gelu_bwd);
   m.def("dropout_bwd", &dropout_bwd);
   m.def("bias_grad", &bias_grad);
+  m.def("dropout_bias_grad", &dropout_bias_grad);
   m.def("gemm", &gemm);
   m.def("gemm_set_variant", &mg::gemm_set_variant);
   m.def("gemm_get_variant", &mg::gemm_get_variant);

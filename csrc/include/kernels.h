@@ -47,6 +47,8 @@ void bias_dropout_residual(const bf16_t* x, const bf16_t* b, const bf16_t* r, bf
 void gelu_bwd(const bf16_t* dy, const bf16_t* pre, bf16_t* dx, long n, hipStream_t stream);
 void dropout_bwd(const bf16_t* dy, bf16_t* dx, long n, float p, uint64_t seed, hipStream_t stream);
 void bias_grad(const bf16_t* dy, float* db, long M, int N, hipStream_t stream);
+void dropout_bias_grad(const bf16_t* dy, bf16_t* dx, float* db, long M, int N, float p, uint64_t seed,
+                       hipStream_t stream);
 
 // gemm.hip -- layout 0 NT (fwd), 1 NN (dgrad), 2 TN (wgrad, fp32 accumulate)
 // epi: 0 none, 1 bias, 2 bias+gelu (pre -> aux), 3 resid + dropout(acc + bias), 4 acc*gelu'(aux)

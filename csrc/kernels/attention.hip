@@ -254,27 +254,32 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
 }
 
 // =============================================================================== backward
-// delta[(b*H + h)*T + t] = sum_d dO * O.  Thread i covers (b, t, h) with h fastest, so a wave
-// reads contiguous 128-B head rows of consecutive heads (coalesced), not rows D*2 bytes apart.
+// delta[(b*H + h)*T + t] = sum_d dO * O.  One lane per 16-byte chunk (8 elements) of a head row,
+// lanes of consecutive chunks/heads/tokens read contiguous memory; the hd/8 lanes of a head row
+// are reduced with xor-shuffles (hd/8 is a power of two <= 8).
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restrict__ dout,
                                                            const bf16_t* __restrict__ out,
                                                            float* __restrict__ delta, int B, int T,
                                                            int H, int hd, int D) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;  // over B*T*H
-  if (i >= (long)B * H * T) return;
-  const int hh = (int)(i % H);
-  const long bt = i / H;
-  const int t = (int)(bt % T), b = (int)(bt / T);
-  const long off = bt * D + hh * hd;
+  const int cpr = hd >> 3;  // chunks per head row: 1, 2, 4 or 8
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;  // over B*T*D/8 chunks
+  const long nchunks = (long)B * T * D / 8;
   float s = 0.f;
-  for (int d = 0; d < hd; d += 8) {
+  if (i < nchunks) {
     float x[8], y[8];
-    unpack8(ld16(dout + off + d), x);
-    unpack8(ld16(out + off + d), y);
+    unpack8(ld16(dout + i * 8), x);
+    unpack8(ld16(out + i * 8), y);
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += x[j] * y[j];
   }
-  delta[((long)b * H + hh) * T + t] = s;
+  for (int o = 1; o < cpr; o <<= 1) s += __shfl_xor(s, o, 64);
+  if (i < nchunks && (i & (cpr - 1)) == 0) {
+    const long e = i * 8;  // element index in [B*T, D]
+    const long bt = e / D;
+    const int hh = (int)((e % D) / hd);
+    const int t = (int)(bt % T), b = (int)(bt / T);
+    delta[((long)b * H + hh) * T + t] = s;
+  }
 }
 
 constexpr int BQ = 64;  // queries per bwd tile
@@ -610,8 +615,8 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
   a.qkv = qkv; a.out = dqkv; a.lse = const_cast<float*>(lse); a.dout = dout; a.delta = delta;
   a.dq = dq; a.dqkv = dqkv; a.dmask = const_cast<uint32_t*>(dmask);
   if (a.thr && !dmask) a.thr = 0;
-  const long bht = (long)B * H * T;
-  attn_bwd_pre_kernel<<<cdiv(bht, 256), 256, 0, stream>>>(dout, out, delta, B, T, H, hd, H * hd);
+  const long nchunks = (long)B * T * H * hd / 8;
+  attn_bwd_pre_kernel<<<cdiv(nchunks, 256), 256, 0, stream>>>(dout, out, delta, B, T, H, hd, H * hd);
   hipMemsetAsync(dq, 0, sizeof(float) * (size_t)B * T * H * hd, stream);
   const int grid = cdiv(T, 128) * B * H;
   if (hd > 32) attn_bwd_kernel<4><<<grid, 256, BWD_SMEM, stream>>>(a);

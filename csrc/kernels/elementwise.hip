@@ -88,6 +88,37 @@ __global__ __launch_bounds__(256) void dropout_bwd_kernel(const bf16_t* __restri
   }
 }
 
+// Same row/column decomposition as bias_grad_kernel below, fused with the residual-dropout
+// backward: dx = dy * mask / (1-p) is written and its column sums are accumulated in one pass.
+__global__ __launch_bounds__(256) void dropout_bias_grad_kernel(const bf16_t* __restrict__ dy,
+                                                                bf16_t* __restrict__ dx,
+                                                                float* __restrict__ db, int M, int N,
+                                                                uint64_t seed, uint32_t thr,
+                                                                float scale) {
+  __shared__ __attribute__((aligned(16))) float red[4][512];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 512 + lane * 8;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c < N) {
+    for (long r = (long)blockIdx.y * 4 + w; r < M; r += (long)gridDim.y * 4) {
+      float g[8];
+      const long e = r * N + c;
+      unpack8(ld16(dy + e), g);
+      dropout8(g, seed, (uint64_t)e, thr, scale);
+      st16(dx + e, pack8(g));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += g[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[w][lane * 8 + j] = s[j];
+  __syncthreads();
+  for (int k = threadIdx.x; k < 512; k += 256) {
+    const int col = blockIdx.x * 512 + k;
+    if (col < N) atomicAdd(db + col, red[0][k] + red[1][k] + red[2][k] + red[3][k]);
+  }
+}
+
 // grid = (ceil(N/512), RB); block = 256 (4 waves).  Wave w of block (cx, ry) sums rows
 // r = ry*4 + w, stepping by 4*RB, over columns cx*512 + lane*8 .. +8; LDS folds the 4 waves;
 // one fp32 atomic per column per block-row (RB-way, tiny).
@@ -144,11 +175,20 @@ void dropout_bwd(const bf16_t* dy, bf16_t* dx, long n, float p, uint64_t seed, h
                                                           scale);
 }
 
+void dropout_bias_grad(const bf16_t* dy, bf16_t* dx, float* db, long M, int N, float p, uint64_t seed,
+                       hipStream_t stream) {
+  const int cx = cdiv(N, 512);
+  int ry = (int)std::min<long>(512, (M + 3) / 4);
+  while (cx * ry > 2048 && ry > 1) ry >>= 1;
+  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  dropout_bias_grad_kernel<<<dim3(cx, ry), 256, 0, stream>>>(dy, dx, db, (int)M, N, seed,
+                                                             dropout_threshold(p), scale);
+}
+
 void bias_grad(const bf16_t* dy, float* db, long M, int N, hipStream_t stream) {
   const int cx = cdiv(N, 512);
-  int ry = (int)std::min<long>(256, (M + 3) / 4);
-  // aim for >= 512 blocks in flight
-  while (cx * ry > 2048 && ry > 1) ry >>= 1;
+  int ry = (int)std::min<long>(512, (M + 3) / 4);
+  while (cx * ry > 2048 && ry > 1) ry >>= 1;  // ~2048 blocks: every CU busy, few atomics per column
   bias_grad_kernel<<<dim3(cx, ry), 256, 0, stream>>>(dy, db, (int)M, N);
 }
 

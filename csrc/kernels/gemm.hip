@@ -42,19 +42,21 @@ constexpr int BK = 64;
 constexpr int GROUP_M = 8;
 constexpr uint32_t kOOB = 0xFFFFFFF0u;
 
-template <int BM_, int BN_, int NWM_, int NWN_>
+template <int BM_, int BN_, int NWM_, int NWN_, int STAGES_ = 2>
 struct Cfg {
-  static constexpr int BM = BM_, BN = BN_, NWM = NWM_, NWN = NWN_;
+  static constexpr int BM = BM_, BN = BN_, NWM = NWM_, NWN = NWN_, STAGES = STAGES_;
   static constexpr int NW = NWM * NWN, NT = NW * 64;
   static constexpr int WTM = BM / NWM, WTN = BN / NWN;  // wave tile
   static constexpr int FM = WTM / 16, FN = WTN / 16;    // 16x16 MFMA tiles per wave
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int SMEM = 2 * STAGE;
+  static constexpr int SMEM = STAGES * STAGE;
+  // LDS-DMA wave-instructions one wave issues per K-step (for the counted vmcnt)
+  static constexpr int DMA_PER_STEP = BM / 8 / NW + BN / 8 / NW;
 };
 using T128 = Cfg<128, 128, 2, 2>;
 using T256 = Cfg<256, 256, 2, 4>;
-using T2x1 = Cfg<256, 128, 4, 2>;
+using T2x1 = Cfg<256, 128, 4, 2, 3>;  // 3-stage ring: two K-steps in flight, 144 KiB
 
 struct GemmArgs {
   const bf16_t* A;
@@ -136,8 +138,9 @@ __global__ __launch_bounds__(CF::NT, 2) void gemm_kernel(const GemmArgs args) {
   const int orig = blockIdx.x;
   const int xcd = orig & 7, q8 = nblk >> 3, r8 = nblk & 7;
   const int wgs = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int split = wgs % args.splits;
-  const int wg = wgs / args.splits;
+  const int ntiles = args.tiles_m * args.tiles_n;
+  const int split = wgs / ntiles;  // split slowest: neighbours on an XCD share a K range (L2 reuse)
+  const int wg = wgs % ntiles;
   const int group = GROUP_M * args.tiles_n;
   const int first_m = (wg / group) * GROUP_M;
   const int gm = min(args.tiles_m - first_m, GROUP_M);
@@ -155,16 +158,29 @@ __global__ __launch_bounds__(CF::NT, 2) void gemm_kernel(const GemmArgs args) {
   const int nk = (min(args.K, kbeg + args.kchunk) - kbeg + BK - 1) / BK;
   const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)args.A, 0, args.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)args.B, 0, args.b_bytes, 0x00020000);
-  dma_tile<AK, CF::BM, CF::NW>(smem, rsa, args.lda, m0, args.a_ext, kbeg, args.ka, wid, lane);
-  dma_tile<BKC, CF::BN, CF::NW>(smem + CF::A_BYTES, rsb, args.ldb, n0, args.b_ext, kbeg, args.kb, wid, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // prologue: STAGES-1 tiles in flight
+#pragma unroll
+  for (int st = 0; st < CF::STAGES - 1; ++st) {
+    if (st < nk) {
+      char* dst = smem + st * CF::STAGE;
+      dma_tile<AK, CF::BM, CF::NW>(dst, rsa, args.lda, m0, args.a_ext, kbeg + st * BK, args.ka, wid, lane);
+      dma_tile<BKC, CF::BN, CF::NW>(dst + CF::A_BYTES, rsb, args.ldb, n0, args.b_ext, kbeg + st * BK, args.kb, wid, lane);
+    }
+  }
+  if constexpr (CF::STAGES == 3) {
+    if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CF::DMA_PER_STEP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
   for (int kt = 0; kt < nk; ++kt) {
-    const char* sa = smem + (kt & 1) * CF::STAGE;
+    const char* sa = smem + (kt % CF::STAGES) * CF::STAGE;
     const char* sb = sa + CF::A_BYTES;
-    if (kt + 1 < nk) {  // stage kt+1 was last read in iteration kt-1: free since its barrier
-      char* dst = smem + ((kt + 1) & 1) * CF::STAGE;
-      const int k1 = kbeg + (kt + 1) * BK;
+    const int kn = kt + CF::STAGES - 1;  // tile to issue now
+    if (kn < nk) {  // its stage was last read in iteration kt-1: free since that barrier
+      char* dst = smem + (kn % CF::STAGES) * CF::STAGE;
+      const int k1 = kbeg + kn * BK;
       dma_tile<AK, CF::BM, CF::NW>(dst, rsa, args.lda, m0, args.a_ext, k1, args.ka, wid, lane);
       dma_tile<BKC, CF::BN, CF::NW>(dst + CF::A_BYTES, rsb, args.ldb, n0, args.b_ext, k1, args.kb, wid, lane);
     }
@@ -183,8 +199,15 @@ __global__ __launch_bounds__(CF::NT, 2) void gemm_kernel(const GemmArgs args) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt+1 landed (issuing waves)
-    __syncthreads();                                   // ... and visible to every wave
+    // tile kt+1 must have landed (this wave's DMA), every wave's LDS reads of stage kt retired;
+    // with 3 stages the DMA of tile kt+2 stays in flight across the barrier (counted vmcnt).
+    if constexpr (CF::STAGES == 3) {
+      if (kn < nk) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(CF::DMA_PER_STEP) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
   }
 
   if constexpr (OUTF32) {

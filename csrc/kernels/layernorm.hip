@@ -169,7 +169,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
 
 namespace mg {
 
-int ln_bwd_grid(int M) { return M / 4 < 512 ? (M + 3) / 4 : 512; }
+int ln_bwd_grid(int M) { return M / 4 < 2048 ? (M + 3) / 4 : 2048; }  // 8 waves/CU in flight
 
 #define MG_LN_DISPATCH(KERNEL, ...)                                                   \
   do {                                                                                \

@@ -88,18 +88,24 @@ class TransformerBlockFn(torch.autograd.Function):
         for prm in ctx.params:
             g[id(prm)] = grad_target(prm)
         # ---- MLP: x2 = x1 + drop(gelu(h2 Wfc^T + bfc) Wp^T + bp)
-        dz = C.dropout_bwd(dx2, p_resid, ctx.seeds[2]) if p_resid > 0 else dx2
+        if p_resid > 0:  # dz = dropout'(dx2) and d(bias) in one pass
+            dz = C.dropout_bias_grad(dx2, g[id(bp)][0], p_resid, ctx.seeds[2])
+        else:
+            dz = dx2
+            C.bias_grad(dz, g[id(bp)][0])
         G.gemm_tn_acc(dz, u, g[id(wp)][0])
-        C.bias_grad(dz, g[id(bp)][0])
         dpre = G.gemm_nn(dz, wp, epi="gelu_bwd", aux=pre)
         G.gemm_tn_acc(dpre, h2, g[id(wfc)][0])
         C.bias_grad(dpre, g[id(bfc)][0])
         dh2 = G.gemm_nn(dpre, wfc)
         dx1 = C.layernorm_bwd(dh2, x1, ln2w, mean2, rstd2, g[id(ln2w)][0], g[id(ln2b)][0], dx2)
         # ---- attention: x1 = x + drop(attn(h Wqkv^T + bqkv) Wo^T + bo)
-        dz = C.dropout_bwd(dx1, p_resid, ctx.seeds[1]) if p_resid > 0 else dx1
+        if p_resid > 0:
+            dz = C.dropout_bias_grad(dx1, g[id(bo)][0], p_resid, ctx.seeds[1])
+        else:
+            dz = dx1
+            C.bias_grad(dz, g[id(bo)][0])
         G.gemm_tn_acc(dz, y, g[id(wo)][0])
-        C.bias_grad(dz, g[id(bo)][0])
         dy = G.gemm_nn(dz, wo)
         dqkv = C.attention_bwd(qkv, y, dy, lse, amask, B, T, H, float(p_attn), ctx.seeds[0])
         G.gemm_tn_acc(dqkv, h, g[id(wqkv)][0])

@@ -154,3 +154,7 @@ def test_elementwise():
     db = torch.zeros(N, device=DEV)
     C.bias_grad(dy, db)
     torch.testing.assert_close(db, dy.float().sum(0), atol=2e-2, rtol=1e-3)
+    db2 = torch.zeros(N, device=DEV)
+    dx2 = C.dropout_bias_grad(dy, db2, 0.5, 7)
+    torch.testing.assert_close(dx2.float(), dx.float())
+    torch.testing.assert_close(db2, dx.float().sum(0), atol=2e-2, rtol=1e-3)
