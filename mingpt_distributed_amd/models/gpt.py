@@ -142,6 +142,15 @@ class GPT(nn.Module):
             n -= self.transformer.wpe.weight.numel()
         return n
 
+    def flops_per_token(self, seq_len: Optional[int] = None) -> float:
+        """Training FLOPs per token (fwd + bwd = 3x fwd), matmuls only: 6 * (non-embedding params
+        + lm_head) + 6 * L * T * d for causal attention (QK^T and PV, half the square each)."""
+        c = self.config
+        T = seq_len or c.block_size
+        n_mm = sum(p.numel() for n, p in self.transformer.h.named_parameters() if p.dim() == 2)
+        n_mm += self.lm_head.weight.numel()
+        return 6.0 * n_mm + 6.0 * c.n_layer * T * c.n_embed
+
     @staticmethod
     def _init_weights(module):
         if isinstance(module, nn.Linear):

@@ -61,6 +61,15 @@ def init_distributed(device: str = "auto", backend: str = "auto", timeout_s: int
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kw["device_id"] = dev
+        restart = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
+        if restart > 0 and "MASTER_PORT" in os.environ:
+            # A restarted worker group shares torchrun's store with the dead one; without a
+            # per-attempt prefix a rank can read a dead peer's gloo address / RCCL unique id
+            # and fail to connect (or hang).  Namespace the bootstrap keys by attempt.
+            agent_store = os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true"
+            base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
+                                 is_master=(rank == 0 and not agent_store), timeout=kw["timeout"])
+            kw.update(store=dist.PrefixStore(f"mingpt/attempt{restart}", base), rank=rank, world_size=world)
         dist.init_process_group(**kw)
     _INFO = DistInfo(rank=rank, world_size=world, local_rank=local, device=dev,
                      backend=backend if world > 1 else "none")

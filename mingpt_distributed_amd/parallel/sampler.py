@@ -23,14 +23,18 @@ class DistributedSampler(Sampler):
         self.num_replicas, self.rank = num_replicas, rank
         self.shuffle, self.seed, self.drop_last = shuffle, seed, drop_last
         self.epoch = 0
+        self.start = 0
         if drop_last:
             self.num_samples = self.n // num_replicas
         else:
             self.num_samples = math.ceil(self.n / num_replicas)
         self.total_size = self.num_samples * num_replicas
 
-    def set_epoch(self, epoch: int) -> None:
+    def set_epoch(self, epoch: int, start: int = 0) -> None:
+        """Select the epoch's permutation; ``start`` skips this rank's first ``start`` samples
+        (mid-epoch resume from a step-granular snapshot)."""
         self.epoch = epoch
+        self.start = start
 
     def __iter__(self) -> Iterator[int]:
         if self.shuffle:
@@ -44,10 +48,10 @@ class DistributedSampler(Sampler):
             idx += (idx * math.ceil(pad / max(1, len(idx))))[:pad]
         else:
             idx = idx[: self.total_size]
-        return iter(idx[self.rank: self.total_size: self.num_replicas])
+        return iter(idx[self.rank: self.total_size: self.num_replicas][self.start:])
 
     def __len__(self) -> int:
-        return self.num_samples
+        return self.num_samples - self.start
 
 
 class InfiniteRandomSampler(Sampler):

@@ -69,6 +69,7 @@ class StepEngine:
             if D.is_initialized() and torch.distributed.get_world_size() > 1 else None
         self.world = self.dp.world if self.dp else 1
         self._hooks = []
+        self.annotate = False  # record_function ranges (fwd/bwd/allreduce/optim) while profiling
         if self.dp is None:
             # single process: ops that return ordinary autograd grads (the CPU reference path)
             # are folded into the fp32 main-grad buffer the optimizer reads
@@ -100,18 +101,25 @@ class StepEngine:
     def to_device(self, t: torch.Tensor) -> torch.Tensor:
         return t.to(self.device, non_blocking=True)
 
+    def _range(self, name: str):
+        return torch.profiler.record_function(name) if self.annotate else contextlib.nullcontext()
+
     def forward_backward(self, x, y, scale: float = 1.0, sync: bool = True):
         ctx = self.dp.no_sync() if (self.dp is not None and not sync) else contextlib.nullcontext()
         with ctx:
-            _, loss = self.model(x, y)
-            (loss * scale if scale != 1.0 else loss).backward()
+            with self._range("mingpt::forward"):
+                _, loss = self.model(x, y)
+            with self._range("mingpt::backward"):
+                (loss * scale if scale != 1.0 else loss).backward()
             if self.dp is not None:
-                self.dp.finish()
+                with self._range("mingpt::allreduce_wait"):
+                    self.dp.finish()
         return loss.detach()
 
     def optimizer_step(self):
-        self.opt.step(grad_scale=1.0 / self.world)
-        self.store.zero_grad()
+        with self._range("mingpt::optimizer"):
+            self.opt.step(grad_scale=1.0 / self.world)
+            self.store.zero_grad()
 
     def train_step(self, batches) -> torch.Tensor:
         """One optimizer step over a list of (x, y) micro-batches; returns the mean loss (device)."""
@@ -166,14 +174,33 @@ class GPTTrainerConfig:
     grad_accum_steps: int = 1
     max_steps_per_epoch: Optional[int] = None
     seed: int = 0
+    save_every_steps: Optional[int] = None      # step-granular snapshots (mid-epoch resume)
+    fault_inject_step: Optional[int] = None     # test hook: fail after this global step
+    fault_inject_rank: Optional[int] = None     # ... on this rank only (None = every rank)
+    fault_inject_mode: str = "raise"            # "raise" (InjectedFault) or "exit" (os._exit(13))
+    metrics_path: Optional[str] = None          # rank-0 JSONL: loss, tokens/s, MFU, grad_norm, lr
+    profile_dir: Optional[str] = None           # torch.profiler (roctracer) trace of a step window
+    profile_steps: str = "3:6"                  # [start, end) global steps traced
+    peak_tflops: float = 2500.0                 # per-GPU dense bf16 peak used for MFU
+
+
+class InjectedFault(RuntimeError):
+    """Raised by ``fault_inject_step``: a deterministic worker failure to test resume."""
 
 
 @dataclass
 class ModelSnapshot:
+    """Reference schema (``/root/reference/mingpt/trainer.py:33-37``) plus step-granular state.
+
+    ``final_epoch`` is the epoch the snapshot was taken in; ``epoch_step`` > 0 marks a mid-epoch
+    snapshot (that many optimizer steps of ``final_epoch`` done), 0 a completed epoch.
+    ``rng_state`` is torch's CPU generator (dropout seeds and data order derive from it)."""
     model_state: "Dict[str, torch.Tensor]"
     optimizer_state: Dict[str, Any]
     final_epoch: int
     step: int = 0
+    epoch_step: int = 0
+    rng_state: Optional[torch.Tensor] = None
 
 
 def _atomic_save(obj, path: str):
@@ -216,7 +243,12 @@ class GPTTrainer:
         self.save_every = config.save_every or 1
         self.last_epoch = -1
         self.step = 0
+        self.resume_epoch_step = 0
         self.history: List[Dict[str, float]] = []
+        self._metrics_f = None
+        self._prof = None
+        self._pending_rng = None
+        self._flops_per_token = model.flops_per_token() if hasattr(model, "flops_per_token") else None
         self._load_snapshot()
 
     # ------------------------------------------------------------------ data
@@ -228,10 +260,10 @@ class GPTTrainer:
                           num_workers=self.config.dl_num_workers or 0, drop_last=True)
 
     # ------------------------------------------------------------------ snapshots
-    def _snapshot_dict(self, epoch: int) -> Dict[str, Any]:
+    def _snapshot_dict(self, epoch: int, epoch_step: int = 0) -> Dict[str, Any]:
         snap = ModelSnapshot(model_state=self.engine.model_state_dict(),
                              optimizer_state=self.engine.opt.state_dict(), final_epoch=epoch,
-                             step=self.step)
+                             step=self.step, epoch_step=epoch_step, rng_state=torch.get_rng_state())
         return asdict(snap)
 
     def _upload_snapshot(self, snapshot, dst: str):
@@ -249,14 +281,16 @@ class GPTTrainer:
             client = boto3.client("s3")
         client.upload_fileobj(buffer, u.netloc, u.path.lstrip("/"))
 
-    def _save_snapshot(self, epoch: int) -> None:
-        snapshot = self._snapshot_dict(epoch)
+    def _save_snapshot(self, epoch: int, epoch_step: int = 0) -> None:
+        # every rank must take part in nothing here: called on global rank 0 only (D19)
+        snapshot = self._snapshot_dict(epoch, epoch_step)
         path = self.config.snapshot_path
         if path.startswith("s3://"):
             self._upload_snapshot(snapshot, path)
         else:
             _atomic_save(snapshot, path)
-        print(f"Model snapshot taken and saved at epoch {epoch}")
+        where = f"epoch {epoch}" + (f" step {epoch_step}" if epoch_step else "")
+        print(f"Model snapshot taken and saved at {where}")
 
     def _load_snapshot(self):
         import fsspec
@@ -271,10 +305,66 @@ class GPTTrainer:
         snap = ModelSnapshot(**data)
         self.engine.load_model_state_dict(snap.model_state)
         self.engine.opt.load_state_dict(snap.optimizer_state)
-        self.last_epoch = snap.final_epoch
         self.step = snap.step
+        # applied once the resumed epoch's DataLoader iterator exists (creating it draws a seed)
+        self._pending_rng = snap.rng_state
+        if snap.epoch_step > 0:  # mid-epoch snapshot: finish that epoch first
+            self.last_epoch = snap.final_epoch - 1
+            self.resume_epoch_step = snap.epoch_step
+        else:
+            self.last_epoch = snap.final_epoch
         if self.global_rank == 0:
-            print(f"Resuming training from epoch {self.last_epoch + 1}")
+            print(f"Resuming training from epoch {self.last_epoch + 1}"
+                  + (f" step {self.resume_epoch_step}" if self.resume_epoch_step else ""))
+
+    # ------------------------------------------------------------------ observability
+    def _log_metrics(self, rec: Dict[str, Any]) -> None:
+        if self.global_rank != 0 or not self.config.metrics_path:
+            return
+        import json
+
+        if self._metrics_f is None:
+            d = os.path.dirname(self.config.metrics_path)
+            if d:
+                os.makedirs(d, exist_ok=True)
+            self._metrics_f = open(self.config.metrics_path, "a")
+        self._metrics_f.write(json.dumps(rec) + "\n")
+        self._metrics_f.flush()
+
+    def _profile_tick(self) -> None:
+        """Start/stop a torch.profiler window over global steps [start, end) (rank 0)."""
+        if not self.config.profile_dir or self.global_rank != 0:
+            return
+        a, b = (int(v) for v in self.config.profile_steps.split(":"))
+        if self.step == a and self._prof is None:
+            acts = [torch.profiler.ProfilerActivity.CPU]
+            if self.engine.device.type == "cuda":
+                acts.append(torch.profiler.ProfilerActivity.CUDA)
+            self._prof = torch.profiler.profile(activities=acts, record_shapes=False)
+            self._prof.__enter__()
+            self.engine.annotate = True
+        elif self.step == b and self._prof is not None:
+            self._prof.__exit__(None, None, None)
+            self.engine.annotate = False
+            os.makedirs(self.config.profile_dir, exist_ok=True)
+            self._prof.export_chrome_trace(os.path.join(self.config.profile_dir, "trace.json"))
+            sort = "cuda_time_total" if self.engine.device.type == "cuda" else "cpu_time_total"
+            with open(os.path.join(self.config.profile_dir, "summary.txt"), "w") as f:
+                f.write(self._prof.key_averages().table(sort_by=sort, row_limit=50))
+            self._prof = None
+
+    def _maybe_inject_fault(self) -> None:
+        c = self.config
+        if c.fault_inject_step is None or self.step != c.fault_inject_step:
+            return
+        if c.fault_inject_rank is not None and c.fault_inject_rank != self.global_rank:
+            return
+        if int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")) > 0:
+            return  # the restarted worker group runs clean (elastic-recovery test)
+        print(f"[GPU{self.global_rank}] injected fault after step {self.step}", flush=True)
+        if c.fault_inject_mode == "exit":
+            os._exit(13)  # a hard worker death: torchrun sees a failed rank
+        raise InjectedFault(f"injected fault after step {self.step}")
 
     # ------------------------------------------------------------------ loops
     def _run_batch(self, inputs, labels, train: bool = True) -> torch.Tensor:
@@ -285,28 +375,53 @@ class GPTTrainer:
         return loss.detach()
 
     def _run_epoch(self, epoch: int, dataloader: DataLoader, train: bool = True) -> float:
+        skip = self.resume_epoch_step if train else 0
         if isinstance(dataloader.sampler, DistributedSampler):
-            dataloader.sampler.set_epoch(epoch)
+            dataloader.sampler.set_epoch(epoch, start=skip * (self.config.batch_size or 1))
         self.model.train(train)
         total, count = None, 0
-        t0 = time.perf_counter()
-        for idx, (x, y) in enumerate(dataloader):
-            if train and self.config.max_steps_per_epoch and idx >= self.config.max_steps_per_epoch:
+        t0 = tlog = time.perf_counter()
+        nlog = 0
+        c = self.config
+        it = iter(dataloader)
+        if train and self._pending_rng is not None:
+            torch.set_rng_state(self._pending_rng)
+            self._pending_rng = None
+        for i, (x, y) in enumerate(it):
+            idx = i + skip
+            if train and c.max_steps_per_epoch and idx >= c.max_steps_per_epoch:
                 break
+            if train:
+                self._profile_tick()
             loss = self._run_batch(x, y, train)
             total = loss if total is None else total + loss
             count += 1
+            nlog += 1
             if train:
                 self.step += 1
-            if idx % self.config.log_every == 0:
-                lg = D.all_reduce_mean(loss.float()).item()
+                if c.save_every_steps and self.step % c.save_every_steps == 0 and self.global_rank == 0:
+                    self._save_snapshot(epoch, epoch_step=idx + 1)
+                self._maybe_inject_fault()
+            if idx % c.log_every == 0:
+                lg = D.all_reduce_mean(loss.float()).item()   # syncs the device: timing is honest
+                now = time.perf_counter()
                 if self.global_rank == 0:
-                    dt = time.perf_counter() - t0
-                    tok = x.numel() * self.world * (idx + 1) / max(dt, 1e-9)
+                    dt = now - tlog
+                    tok_s = x.numel() * self.world * nlog / max(dt, 1e-9)
                     gn = self.engine.grad_norm.item() if train else float("nan")
                     print(f"[GPU{self.global_rank}] Epoch {epoch} | Iter {idx} | "
                           f"{'Training' if train else 'Test'} loss {lg:.5f} | grad_norm {gn:.3f} | "
-                          f"{tok:,.0f} tok/s", flush=True)
+                          f"{tok_s:,.0f} tok/s", flush=True)
+                    rec = {"epoch": epoch, "iter": idx, "step": self.step, "split": "train" if train else "test",
+                           "loss": lg, "tokens_per_s": tok_s, "step_ms": dt / nlog * 1e3}
+                    if train:
+                        rec.update(grad_norm=gn, lr=self.engine.lr)
+                        if self._flops_per_token and self.engine.device.type == "cuda":
+                            rec["mfu"] = tok_s * self._flops_per_token / (self.world * c.peak_tflops * 1e12)
+                    self._log_metrics(rec)
+                tlog, nlog = now, 0
+        if train:
+            self.resume_epoch_step = 0
         if count == 0:
             return float("nan")
         mean = D.all_reduce_mean((total / count).float()).item()
@@ -315,15 +430,24 @@ class GPTTrainer:
 
     def train(self) -> None:
         start = self.last_epoch + 1
-        for epoch in range(start, self.config.max_epochs):
-            tr = self._run_epoch(epoch, self.train_loader, True)
-            rec = {"epoch": epoch, "train_loss": tr}
-            if self.global_rank == 0 and epoch % self.save_every == 0:
-                self._save_snapshot(epoch)
-            if self.test_loader is not None:
-                rec["test_loss"] = self._run_epoch(epoch, self.test_loader, False)
-            self.history.append(rec)
-            D.barrier()
+        try:
+            for epoch in range(start, self.config.max_epochs):
+                tr = self._run_epoch(epoch, self.train_loader, True)
+                rec = {"epoch": epoch, "train_loss": tr}
+                if self.global_rank == 0 and epoch % self.save_every == 0:
+                    self._save_snapshot(epoch)
+                if self.test_loader is not None:
+                    rec["test_loss"] = self._run_epoch(epoch, self.test_loader, False)
+                self.history.append(rec)
+                self._log_metrics(dict(rec, split="epoch"))
+                D.barrier()
+        finally:
+            if self._prof is not None:
+                self._prof.__exit__(None, None, None)
+                self._prof = None
+            if self._metrics_f is not None:
+                self._metrics_f.close()
+                self._metrics_f = None
 
 
 # ====================================================================================== upstream

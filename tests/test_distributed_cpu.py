@@ -102,3 +102,37 @@ def _worker_trainer(rank, world, port, out_dir):
 def test_gpt_trainer_two_ranks(tmp_path):
     mp.spawn(_worker_trainer, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
     assert os.path.exists(tmp_path / "s.pt")
+
+
+def test_torchrun_elastic_restart_resumes_from_step_snapshot(tmp_path):
+    """rank 1 dies hard (os._exit) after step 7; torchrun (--max-restarts 1) restarts
+    the worker group, which resumes from the step-5 snapshot and finishes the run.  c10d rendezvous
+    (as ``scripts/run_node.sh`` / the reference ``slurm_run.sh:17-22`` use): a static-port restart
+    can reconnect gloo to the dead group's stale addresses."""
+    import subprocess
+    import sys
+
+    corpus = tmp_path / "input.txt"
+    corpus.write_text("the quick brown fox jumps over the lazy dog. " * 60)
+    cfg = tmp_path / "cfg.yaml"
+    cfg.write_text(f"""
+gpt_config: {{n_layer: 1, n_head: 2, n_embd: 32}}
+optimizer_config: {{learning_rate: 0.001}}
+data_config: {{path: {corpus}, block_size: 16}}
+trainer_config: {{max_epochs: 1, batch_size: 8, grad_norm_clip: 1.0, snapshot_path: {tmp_path / 's.pt'},
+                 save_every: 1, max_steps_per_epoch: 12, log_every: 1000, save_every_steps: 5,
+                 fault_inject_step: 7, fault_inject_rank: 1, fault_inject_mode: exit}}
+""")
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("TORCHELASTIC_RESTART_COUNT", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--max-restarts", "1", "--rdzv-backend", "c10d", "--rdzv-endpoint", f"127.0.0.1:{_port()}",
+           "-m", "mingpt_distributed_amd.train", "--config", str(cfg), "--device", "cpu"]
+    r = subprocess.run(cmd, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), env=env,
+                       capture_output=True, text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    assert "injected fault after step 7" in out
+    assert "Resuming training from epoch 0 step 5" in out
+    snap = torch.load(str(tmp_path / "s.pt"), weights_only=True)
+    assert snap["step"] == 12 and snap["final_epoch"] == 0 and snap["epoch_step"] == 0

@@ -75,7 +75,7 @@ def test_s3_upload_with_injected_client(tmp_path):
         GPTTrainer.s3_client_factory = None
     blob = uploads[("bucket", "run/gpt_snapshot.pt")]
     snap = torch.load(io.BytesIO(blob), weights_only=True)
-    assert set(snap) == {"model_state", "optimizer_state", "final_epoch", "step"}
+    assert set(snap) == {"model_state", "optimizer_state", "final_epoch", "step", "epoch_step", "rng_state"}
 
 
 def test_upstream_trainer_api_sort_task():
@@ -115,3 +115,64 @@ trainer_config: {{max_epochs: 1, batch_size: 8, grad_norm_clip: 1.0, snapshot_pa
 """)
     tr = main(["--config", str(cfgp), "--device", "cpu", "trainer_config.log_every=1"])
     assert tr.history and os.path.exists(tmp_path / "s.pt")
+
+
+def _final_params(model):
+    return {n: p.detach().clone() for n, p in model.named_parameters()}
+
+
+def test_fault_injection_and_step_granular_resume(tmp_path):
+    """A run killed mid-epoch by the fault hook and resumed from its step snapshot ends with the
+    same weights as an uninterrupted run (data order, dropout RNG and optimizer state restored)."""
+    from mingpt_distributed_amd.trainer import InjectedFault
+
+    def run(snapshot, **kw):
+        cfg, model, opt, train, _ = _setup(tmp_path, snapshot=snapshot, max_epochs=2)
+        model.config  # dropout 0.1 stays on: the RNG state must be restored for equality
+        for k, v in kw.items():
+            setattr(cfg, k, v)
+        tr = GPTTrainer(cfg, model, opt, train, None)
+        tr.train()
+        return tr
+
+    ref = run("ref.pt", save_every_steps=1000)
+    with pytest.raises(InjectedFault):
+        run("ft.pt", save_every_steps=5, fault_inject_step=27)
+    snap = torch.load(str(tmp_path / "ft.pt"), weights_only=True)
+    assert snap["step"] == 25 and snap["final_epoch"] == 1 and snap["epoch_step"] == 5
+    resumed = run("ft.pt", save_every_steps=5)
+    assert resumed.step == ref.step == 40
+    a, b = _final_params(ref.model), _final_params(resumed.model)
+    for n in a:
+        torch.testing.assert_close(a[n], b[n], rtol=0, atol=0, msg=n)
+
+
+def test_metrics_jsonl_and_profiler(tmp_path):
+    import json
+
+    cfg, model, opt, train, test = _setup(tmp_path, max_epochs=1)
+    cfg.log_every = 5
+    cfg.metrics_path = str(tmp_path / "m" / "metrics.jsonl")
+    cfg.profile_dir = str(tmp_path / "prof")
+    cfg.profile_steps = "2:4"
+    tr = GPTTrainer(cfg, model, opt, train, test)
+    tr.train()
+    recs = [json.loads(l) for l in open(cfg.metrics_path)]
+    steps = [r for r in recs if r["split"] == "train"]
+    assert [r["iter"] for r in steps] == [0, 5, 10, 15]
+    assert all(r["tokens_per_s"] > 0 and r["lr"] > 0 and r["grad_norm"] >= 0 for r in steps)
+    assert recs[-1]["split"] == "epoch" and "test_loss" in recs[-1]
+    assert os.path.exists(tmp_path / "prof" / "trace.json")
+    summary = open(tmp_path / "prof" / "summary.txt").read()
+    assert "mingpt::forward" in summary and "mingpt::optimizer" in summary
+    assert not tr.engine.annotate
+
+
+def test_sampler_mid_epoch_start():
+    from mingpt_distributed_amd.parallel.sampler import DistributedSampler
+
+    s = DistributedSampler(list(range(100)), num_replicas=2, rank=1, shuffle=True, seed=3)
+    s.set_epoch(4)
+    full = list(s)
+    s.set_epoch(4, start=10)
+    assert list(s) == full[10:] and len(s) == len(full) - 10
