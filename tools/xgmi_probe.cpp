@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unistd.h>
 #include <vector>
 
 #define HIPCHECK(x)                                                                          \
@@ -88,7 +89,10 @@ int main(int argc, char** argv) {
   HIPCHECK(hipGetDeviceCount(&n));
   int ver = 0;
   NCCLCHECK(ncclGetVersion(&ver));
-  printf("xgmi_probe: %d GPU(s), RCCL %d\n", n, ver);
+  char host[256] = {0};
+  gethostname(host, sizeof(host) - 1);
+  const char* node = getenv("SLURM_NODEID");
+  printf("xgmi_probe on %s (node %s): %d GPU(s), RCCL %d\n", host, node ? node : "0", n, ver);
   std::vector<std::string> bus(n);
   for (int d = 0; d < n; ++d) {
     hipDeviceProp_t p;
@@ -169,7 +173,7 @@ int main(int argc, char** argv) {
     HIPCHECK(hipStreamCreate(&streams[d]));
     int rank = 0;
     NCCLCHECK(ncclCommUserRank(comms[d], &rank));
-    printf("hello from rank %d on GPU %d (%s)\n", rank, d, bus[d].c_str());
+    printf("hello from rank %d on GPU %d (%s) of %s\n", rank, d, bus[d].c_str(), host);
   }
   // correctness: rank r contributes (r + 1); expect n(n+1)/2 everywhere
   const size_t cnt = 1 << 20;
