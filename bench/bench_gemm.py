@@ -14,6 +14,9 @@ import torch
 from mingpt_distributed_amd.ops import gemm as G
 
 
+VARIANTS = ("auto", "t128", "t256", "t256x128", "pp256", "w4")
+
+
 def timeit(fn, iters=20, warm=3):
     for _ in range(warm):
         fn()
@@ -40,9 +43,9 @@ def main():
     rows = []
     C = __import__("mingpt_distributed_amd.ops._ext", fromlist=["ext"]).ext()
 
-    def both(fn):  # A/B the tile configs of the hand-written kernel in one process (auto, 128, 256, 256x128)
+    def both(fn):  # A/B the tile configs of the hand-written kernel in one process
         out = []
-        for v in (0, 1, 2, 3):
+        for v in range(len(VARIANTS)):
             C.gemm_set_variant(v)
             out.append(timeit(fn))
         C.gemm_set_variant(0)
@@ -79,14 +82,13 @@ def main():
                           "hipblaslt_tflops": round(fl / tb / 1e9, 1), "speedup": round(tb / tm, 3)}),
               flush=True)
     print(json.dumps({"total_mine_ms": round(tot_m, 3), "total_hipblaslt_ms": round(tot_b, 3)}))
-    print(json.dumps({"variant_ms(auto,t128,t256,t256x128)": {f"{k[0]}:{k[1]}": [round(t, 4) for t in v] for k, v in variants.items()}}))
-    n = 4096
-    a4, b4 = r(n, n), r(n, n)
-    t4, v4 = both(lambda: G.gemm_nt(a4, b4))
-    tb4 = timeit(lambda: torch.mm(a4, b4.t()))
-    print(json.dumps({"gemm_4096^3_tflops": {k: round(2 * n ** 3 / t / 1e9, 1) for k, t in
-                                              zip(("auto", "t128", "t256", "t256x128"), v4)} |
-                      {"hipblaslt": round(2 * n ** 3 / tb4 / 1e9, 1)}}))
+    print(json.dumps({"variant_ms(" + ",".join(VARIANTS) + ")": {f"{k[0]}:{k[1]}": [round(t, 4) for t in v] for k, v in variants.items()}}))
+    for n in (4096, 8192):
+        a4, b4 = r(n, n), r(n, n)
+        t4, v4 = both(lambda: G.gemm_nt(a4, b4))
+        tb4 = timeit(lambda: torch.mm(a4, b4.t()))
+        print(json.dumps({f"gemm_{n}^3_tflops": {k: round(2 * n ** 3 / t / 1e9, 1) for k, t in zip(VARIANTS, v4)} |
+                          {"hipblaslt": round(2 * n ** 3 / tb4 / 1e9, 1)}}))
 
 
 if __name__ == "__main__":

@@ -197,12 +197,14 @@ at::Tensor gelu_bwd(const at::Tensor& dy, const at::Tensor& pre) {
   return dx;
 }
 
+// residual-stream dropout backward: the mask is keyed on (row, column) of the [.., N] tensor
 at::Tensor dropout_bwd(const at::Tensor& dy, double p, int64_t seed) {
   CHECK_BF16(dy); CHECK_CONTIG(dy);
-  TORCH_CHECK(dy.numel() % 8 == 0);
+  const int64_t N = dy.size(-1), M = dy.numel() / N;
+  TORCH_CHECK(N % 8 == 0, "dropout_bwd: last dim must be a multiple of 8");
   DevGuard g(dy.device());
   auto dx = at::empty_like(dy);
-  mg::dropout_bwd(bp(dy), bp(dx), dy.numel(), (float)p, (uint64_t)seed, cur_stream());
+  mg::dropout_bwd(bp(dy), bp(dx), M, (int)N, (float)p, (uint64_t)seed, cur_stream());
   return dx;
 }
 

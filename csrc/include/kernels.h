@@ -45,7 +45,7 @@ void bias_act_fwd(const bf16_t* x, const bf16_t* b, bf16_t* pre, bf16_t* y, long
 void bias_dropout_residual(const bf16_t* x, const bf16_t* b, const bf16_t* r, bf16_t* y, long M,
                            int N, float p, uint64_t seed, hipStream_t stream);
 void gelu_bwd(const bf16_t* dy, const bf16_t* pre, bf16_t* dx, long n, hipStream_t stream);
-void dropout_bwd(const bf16_t* dy, bf16_t* dx, long n, float p, uint64_t seed, hipStream_t stream);
+void dropout_bwd(const bf16_t* dy, bf16_t* dx, long M, int N, float p, uint64_t seed, hipStream_t stream);
 void bias_grad(const bf16_t* dy, float* db, long M, int N, hipStream_t stream);
 void dropout_bias_grad(const bf16_t* dy, bf16_t* dx, float* db, long M, int N, float p, uint64_t seed,
                        hipStream_t stream);
@@ -56,7 +56,8 @@ void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long l
           long ldc, int M, int N, int K, int a_ext, int b_ext, int ka, int kb, const bf16_t* bias,
           bf16_t* aux, const bf16_t* resid, float p, uint64_t seed, hipStream_t stream,
           size_t a_bytes, size_t b_bytes);  // operand sizes in bytes (< 4 GiB for the DMA path)
-void gemm_set_variant(int v);  // 0 register staging, 1 LDS-DMA staging (default)
+void gemm_set_variant(int v);  // tile config override: 0 auto (per shape), 1..5 forced (gemm.hip)
+void gemm_set_debug_buffer(unsigned long long* p);  // MG_GEMM_STAMPS diagnostic builds
 int gemm_get_variant();
 
 // attention.hip -- causal flash attention, hd <= 64; qkv [B*T, 3D], out [B*T, D], lse [B*H*T]

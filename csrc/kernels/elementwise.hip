@@ -4,7 +4,7 @@
 //   bias_act_fwd:      y = act(x + b)             act in {identity, gelu}; optionally keeps pre
 //   bias_drop_resid:   y = r + dropout(x + b)     (attn c_proj / mlp c_proj residual epilogue)
 //   gelu_bwd:          dx = dy * gelu'(pre)
-//   dropout_bwd:       dx = dy * mask * 1/(1-p)   (mask regenerated from the Philox seed)
+//   dropout_bwd:       dx = dy * mask * scale     (mask regenerated from the Philox seed; common.h rowdrop)
 //   bias_grad:         db[n] += sum_m dy[m, n]    (fp32 accumulate into the main grad)
 //
 // All tensors are [M, N] bf16 row-major with N % 8 == 0; 8 elements (16 B) per lane.
@@ -44,9 +44,11 @@ __global__ __launch_bounds__(256) void bias_act_kernel(const bf16_t* __restrict_
 __global__ __launch_bounds__(256) void bias_drop_resid_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ b, const bf16_t* __restrict__ r,
     bf16_t* __restrict__ y, long n8, int N, uint64_t seed, uint32_t thr, float scale, int use_drop) {
+  const uint32_t n8row = (uint32_t)(N >> 3);
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
     const long e = i * 8;
-    const int c = (int)(e % N);
+    const long m = (long)((uint64_t)i / n8row);
+    const int c = (int)(e - m * N);
     float v[8], bb[8], rr[8];
     unpack8(ld16(x + e), v);
     if (b) {
@@ -54,7 +56,7 @@ __global__ __launch_bounds__(256) void bias_drop_resid_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += bb[j];
     }
-    if (use_drop) dropout8(v, seed, (uint64_t)e, thr, scale);
+    if (use_drop) rowdrop8(v, seed, m, c, N, thr, scale);
     unpack8(ld16(r + e), rr);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] += rr[j];
@@ -77,13 +79,15 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(const bf16_t* __restrict_
 }
 
 __global__ __launch_bounds__(256) void dropout_bwd_kernel(const bf16_t* __restrict__ dy,
-                                                          bf16_t* __restrict__ dx, long n8,
+                                                          bf16_t* __restrict__ dx, long n8, int N,
                                                           uint64_t seed, uint32_t thr, float scale) {
+  const uint32_t n8row = (uint32_t)(N >> 3);
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
     const long e = i * 8;
+    const long m = (long)((uint64_t)i / n8row);
     float g[8];
     unpack8(ld16(dy + e), g);
-    dropout8(g, seed, (uint64_t)e, thr, scale);
+    rowdrop8(g, seed, m, (int)(e - m * N), N, thr, scale);
     st16(dx + e, pack8(g));
   }
 }
@@ -104,7 +108,7 @@ __global__ __launch_bounds__(256) void dropout_bias_grad_kernel(const bf16_t* __
       float g[8];
       const long e = r * N + c;
       unpack8(ld16(dy + e), g);
-      dropout8(g, seed, (uint64_t)e, thr, scale);
+      rowdrop8(g, seed, r, c, N, thr, scale);
       st16(dx + e, pack8(g));
 #pragma unroll
       for (int j = 0; j < 8; ++j) s[j] += g[j];
@@ -160,19 +164,20 @@ void bias_act_fwd(const bf16_t* x, const bf16_t* b, bf16_t* pre, bf16_t* y, long
 void bias_dropout_residual(const bf16_t* x, const bf16_t* b, const bf16_t* r, bf16_t* y, long M,
                            int N, float p, uint64_t seed, hipStream_t stream) {
   const long n8 = M * N / 8;
-  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  bias_drop_resid_kernel<<<grid_for(n8), 256, 0, stream>>>(x, b, r, y, n8, N, seed,
-                                                           dropout_threshold(p), scale, p > 0.f);
+  const uint32_t thr = dropout_threshold8(p);
+  bias_drop_resid_kernel<<<grid_for(n8), 256, 0, stream>>>(x, b, r, y, n8, N, seed, thr,
+                                                           dropout_scale8(thr), thr > 0);
 }
 
 void gelu_bwd(const bf16_t* dy, const bf16_t* pre, bf16_t* dx, long n, hipStream_t stream) {
   gelu_bwd_kernel<<<grid_for(n / 8), 256, 0, stream>>>(dy, pre, dx, n / 8);
 }
 
-void dropout_bwd(const bf16_t* dy, bf16_t* dx, long n, float p, uint64_t seed, hipStream_t stream) {
-  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  dropout_bwd_kernel<<<grid_for(n / 8), 256, 0, stream>>>(dy, dx, n / 8, seed, dropout_threshold(p),
-                                                          scale);
+void dropout_bwd(const bf16_t* dy, bf16_t* dx, long M, int N, float p, uint64_t seed,
+                 hipStream_t stream) {
+  const uint32_t thr = dropout_threshold8(p);
+  const long n8 = M * N / 8;
+  dropout_bwd_kernel<<<grid_for(n8), 256, 0, stream>>>(dy, dx, n8, N, seed, thr, dropout_scale8(thr));
 }
 
 void dropout_bias_grad(const bf16_t* dy, bf16_t* dx, float* db, long M, int N, float p, uint64_t seed,
@@ -180,9 +185,9 @@ void dropout_bias_grad(const bf16_t* dy, bf16_t* dx, float* db, long M, int N, f
   const int cx = cdiv(N, 512);
   int ry = (int)std::min<long>(512, (M + 3) / 4);
   while (cx * ry > 2048 && ry > 1) ry >>= 1;
-  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  dropout_bias_grad_kernel<<<dim3(cx, ry), 256, 0, stream>>>(dy, dx, db, (int)M, N, seed,
-                                                             dropout_threshold(p), scale);
+  const uint32_t thr = dropout_threshold8(p);
+  dropout_bias_grad_kernel<<<dim3(cx, ry), 256, 0, stream>>>(dy, dx, db, (int)M, N, seed, thr,
+                                                             dropout_scale8(thr));
 }
 
 void bias_grad(const bf16_t* dy, float* db, long M, int N, hipStream_t stream) {

@@ -76,35 +76,91 @@ struct GemmArgs {
   int tiles_m, tiles_n;
   int splits, kchunk;         // split-K (fp32-accumulate layout only): K range per split
   uint32_t a_bytes, b_bytes;  // buffer-resource extents (out-of-range reads return 0)
+  unsigned long long* dbg;    // MG_GEMM_STAMPS diagnostic builds only: per-wave phase timestamps
 };
 
-static int g_variant = 0;  // 0 auto, 1 force T128, 2 force T256, 3 force T2x1
+static unsigned long long* g_dbg = nullptr;  // MG_GEMM_STAMPS builds: stamp buffer
+static int g_variant = 0;  // 0 auto, 1 force T128, 2 force T256, 3 force T2x1, 4 force PP, 5 force W4
 
 MG_DEVICE int swz_mn(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 
-// ---- LDS-DMA staging of one operand tile (R rows/cols of the m|n dimension x BK) by NW waves.
+// ---- Buffer descriptor of K-tile t: base advanced to the tile's first k, extent shrunk with it,
+// so per-lane offsets stay fixed while out-of-range rows (kOOB) and the buffer end still read 0.
+// The inputs are readfirstlane'd: provably uniform, hence no waterfall loop per buffer op.
+MG_DEVICE __amdgpu_buffer_rsrc_t tile_rsrc(const char* base, uint32_t bytes, uint32_t step, int t) {
+  const uint32_t adv = (uint32_t)t * step;
+  const uint64_t p = reinterpret_cast<uint64_t>(base) + adv;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  const uint32_t n = __builtin_amdgcn_readfirstlane(adv < bytes ? bytes - adv : 0u);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+}
+
+// ---- LDS-DMA stager of one operand tile (R rows/cols of the m|n dimension x BK) by NW waves.
 // Each buffer_load ... lds wave-instruction writes 1 KiB at (wave-uniform base + lane*16).
+// Per-lane source offsets are computed once; a K-tile costs one descriptor (SALU) plus, per piece,
+// an M0 write and the load.  Per-lane k checks run only on K-tiles that cross the valid k extent.
 template <bool KC, int R, int NW>
-MG_DEVICE void dma_tile(char* lds, __amdgpu_buffer_rsrc_t rs, long ld, int r0, int ext, int k0,
-                        int kvalid, int wid, int lane) {
-  constexpr int PER = R / 8 / NW;  // 1-KiB blocks per wave (R*128 B per tile)
+struct Stager {
+  static constexpr int PER = R / 8 / NW;  // 1-KiB pieces per wave (R*128 B per tile)
+  uint32_t voff[PER];
+  const char* base;
+  uint32_t bytes, step;
+  int klim, tail_t, swid;
+
+  MG_DEVICE void init(const bf16_t* ptr, uint32_t total, long ld, int r0, int ext, int kbeg, int kvalid,
+                      int kend, int wid, int lane) {
+    const uint32_t k0b = KC ? (uint32_t)kbeg * 2 : (uint32_t)((long)kbeg * ld * 2);
+    base = reinterpret_cast<const char*>(ptr) + k0b;
+    bytes = total > k0b ? total - k0b : 0u;
+    step = KC ? BK * 2 : (uint32_t)(BK * ld * 2);
+    klim = min(kvalid, kend) - kbeg;
+    tail_t = klim / BK;
+    swid = __builtin_amdgcn_readfirstlane(wid);
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int j = wid * PER + i;
-    uint32_t off;
-    if constexpr (KC) {  // [R rows][128 B]: block = 8 rows x 8 chunks
-      const int row = 8 * j + (lane >> 3), ch = (lane & 7) ^ (row & 7);
-      const int gr = r0 + row, gk = k0 + ch * 8;
-      off = (gr < ext && gk < kvalid) ? (uint32_t)(((long)gr * ld + gk) * 2) : kOOB;
-    } else {  // R/128 half-images [64 k][256 B]: block = 4 k-rows x 16 chunks
-      const int half = j >> 4, jj = j & 15;
-      const int row = 4 * jj + (lane >> 4), ch = (lane & 15) ^ swz_mn(row);
-      const int gk = k0 + row, gc = r0 + half * 128 + ch * 8;
-      off = (gk < kvalid && gc < ext) ? (uint32_t)(((long)gk * ld + gc) * 2) : kOOB;
+    for (int i = 0; i < PER; ++i) {
+      const int j = wid * PER + i;
+      if constexpr (KC) {  // [R rows][128 B]: block = 8 rows x 8 chunks
+        const int row = 8 * j + (lane >> 3), ch = (lane & 7) ^ (row & 7);
+        const int gr = r0 + row;
+        voff[i] = gr < ext ? (uint32_t)(((long)gr * ld + ch * 8) * 2) : kOOB;
+      } else {  // R/128 half-images [64 k][256 B]: block = 4 k-rows x 16 chunks
+        const int half = j >> 4, jj = j & 15;
+        const int row = 4 * jj + (lane >> 4), ch = (lane & 15) ^ swz_mn(row);
+        const int gc = r0 + half * 128 + ch * 8;
+        voff[i] = gc < ext ? (uint32_t)(((long)row * ld + gc) * 2) : kOOB;
+      }
+    }
+  }
+  // piece-level form for hand-interleaved schedules: descriptor once per tile, then piece(i)
+  MG_DEVICE __amdgpu_buffer_rsrc_t rsrc(int t) const { return tile_rsrc(base, bytes, step, t); }
+  MG_DEVICE void piece(char* lds, __amdgpu_buffer_rsrc_t rs, int t, int i) const {
+    const int j = swid * PER + i;
+    uint32_t off = voff[i];
+    if (t >= tail_t) {
+      const int lane = threadIdx.x & 63;
+      const int kpos = KC ? ((lane & 7) ^ ((lane >> 3) & 7)) * 8 : 4 * (j & 15) + (lane >> 4);
+      off = kpos < klim - t * BK ? off : kOOB;
     }
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + j * 1024), 16, off, 0, 0, 0);
   }
-}
+  MG_DEVICE void stage(char* lds, int t) const {
+    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(base, bytes, step, t);
+    const bool tail = t >= tail_t;
+    const int kl = klim - t * BK;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int j = swid * PER + i;
+      uint32_t off = voff[i];
+      if (tail) {
+        const int kpos = KC ? ((lane & 7) ^ ((lane >> 3) & 7)) * 8 : 4 * (j & 15) + (lane >> 4);
+        off = kpos < kl ? off : kOOB;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + j * 1024), 16, off, 0, 0, 0);
+    }
+  }
+};
 
 // ---- fragment read for 16-wide subtile sb, k-step ks (32 k)
 template <bool KC>
@@ -124,6 +180,111 @@ MG_DEVICE bf16x8 frag(const char* lds, int sb, int ks, int lane) {
     const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
     const s16x8 v = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
     return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+// Shared epilogue: lane holds acc[i][j] = C[m0+wm*WTM+16i+(lane&15)][n0+wn*WTN+16j+4(lane>>4) .. +3].
+template <class CF, int EPI, bool OUTF32>
+MG_DEVICE void epilogue(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int m0, int n0, int wm,
+                        int wn, int wid, int lane, char* smem) {
+  if constexpr (OUTF32) {
+    if (args.splits > 1) {
+      // split-K: fp32 atomics into C.  Each wave stages its tile through LDS 32 rows at a time
+      // (row stride WTN+4 floats: conflict-free ds_write_b128), then every atomic
+      // wave-instruction adds WTN contiguous floats of one row (256 B: the full-rate shape).
+      constexpr int RS = CF::WTN + 4;
+      float* ct = reinterpret_cast<float*>(smem) + wid * 32 * RS;
+      float* C = reinterpret_cast<float*>(args.C);
+#pragma unroll
+      for (int pass = 0; pass < CF::FM / 2; ++pass) {
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int j = 0; j < CF::FN; ++j)
+            *reinterpret_cast<f32x4*>(ct + (ii * 16 + (lane & 15)) * RS + j * 16 + (lane >> 4) * 4) =
+                acc[pass * 2 + ii][j];
+        __syncthreads();
+        for (int c = lane; c < CF::WTN; c += 64) {
+          const int n = n0 + wn * CF::WTN + c;
+          for (int r = 0; r < 32; ++r) {
+            const int m = m0 + wm * CF::WTM + pass * 32 + r;
+            if (m < args.M && n < args.N) atomicAdd(C + (long)m * args.ldc + n, ct[r * RS + c]);
+          }
+        }
+        __syncthreads();
+      }
+      return;
+    }
+  }
+  // ---- epilogue: lane holds C[m][n..n+3].  Side inputs are loaded a whole row group at a time
+  // (bias once per lane; resid / aux / fp32 C for all FN column groups of row m before any use), so a
+  // tile pays ~FM load latencies instead of FM x FN serialised round trips.
+  const int nlim = (EPI == 0 && !OUTF32) ? (int)args.ldc : args.N;
+  const int nb = n0 + wn * CF::WTN + (lane >> 4) * 4;
+  const bf16_t* __restrict__ bias = args.bias;
+  uint2 bs[CF::FN];
+#pragma unroll
+  for (int j = 0; j < CF::FN; ++j) {
+    bs[j] = make_uint2(0u, 0u);
+    if constexpr (EPI == 1 || EPI == 2 || EPI == 3)
+      if (bias && nb + j * 16 < nlim) bs[j] = *reinterpret_cast<const uint2*>(bias + nb + j * 16);
+  }
+#pragma unroll
+  for (int i = 0; i < CF::FM; ++i) {
+    const int m = m0 + wm * CF::WTM + i * 16 + (lane & 15);
+    if (m >= args.M) continue;
+    const long rowoff = (long)m * args.ldc;
+    uint2 side[CF::FN];
+    float4 cold[OUTF32 ? CF::FN : 1];
+#pragma unroll
+    for (int j = 0; j < CF::FN; ++j) {
+      const int n = nb + j * 16;
+      if (n >= nlim) continue;
+      if constexpr (OUTF32) {
+        cold[j] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(args.C) + rowoff + n);
+      } else if constexpr (EPI == 3) {
+        side[j] = *reinterpret_cast<const uint2*>(args.resid + rowoff + n);
+      } else if constexpr (EPI == 4) {
+        side[j] = *reinterpret_cast<const uint2*>(args.aux + rowoff + n);
+      }
+    }
+    uint4 rnd = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int j = 0; j < CF::FN; ++j) {
+      const int n = nb + j * 16;
+      if (n >= nlim) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      const long off = rowoff + n;
+      if constexpr (OUTF32) {
+        float4 c = cold[j];
+        c.x += v[0]; c.y += v[1]; c.z += v[2]; c.w += v[3];
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(args.C) + off) = c;
+      } else {
+        if constexpr (EPI == 1 || EPI == 2 || EPI == 3) {
+          v[0] += bf2f(bs[j].x & 0xffffu); v[1] += bf2f(bs[j].x >> 16);
+          v[2] += bf2f(bs[j].y & 0xffffu); v[3] += bf2f(bs[j].y >> 16);
+        }
+        if constexpr (EPI == 2) {
+          *reinterpret_cast<uint2*>(args.aux + off) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = gelu_f(v[r]);
+        }
+        if constexpr (EPI == 3) {
+          if (args.thr) {  // one Philox call per 64-column block of this lane's row (common.h rowdrop)
+            if ((j & 3) == 0) rnd = rowdrop_call(args.seed, m, n, args.N);
+            rowdrop4(v, word_of(rnd, j & 3), args.thr, args.scale);
+          }
+          v[0] += bf2f(side[j].x & 0xffffu); v[1] += bf2f(side[j].x >> 16);
+          v[2] += bf2f(side[j].y & 0xffffu); v[3] += bf2f(side[j].y >> 16);
+        }
+        if constexpr (EPI == 4) {
+          v[0] *= gelu_grad(bf2f(side[j].x & 0xffffu)); v[1] *= gelu_grad(bf2f(side[j].x >> 16));
+          v[2] *= gelu_grad(bf2f(side[j].y & 0xffffu)); v[3] *= gelu_grad(bf2f(side[j].y >> 16));
+        }
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(args.C) + off) =
+            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
+    }
   }
 }
 
@@ -156,15 +317,17 @@ __global__ __launch_bounds__(CF::NT, 2) void gemm_kernel(const GemmArgs args) {
 
   const int kbeg = split * args.kchunk;
   const int nk = (min(args.K, kbeg + args.kchunk) - kbeg + BK - 1) / BK;
-  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)args.A, 0, args.a_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)args.B, 0, args.b_bytes, 0x00020000);
+  Stager<AK, CF::BM, CF::NW> sta;
+  Stager<BKC, CF::BN, CF::NW> stb;
+  sta.init(args.A, args.a_bytes, args.lda, m0, args.a_ext, kbeg, args.ka, kbeg + args.kchunk, wid, lane);
+  stb.init(args.B, args.b_bytes, args.ldb, n0, args.b_ext, kbeg, args.kb, kbeg + args.kchunk, wid, lane);
   // prologue: STAGES-1 tiles in flight
 #pragma unroll
   for (int st = 0; st < CF::STAGES - 1; ++st) {
     if (st < nk) {
       char* dst = smem + st * CF::STAGE;
-      dma_tile<AK, CF::BM, CF::NW>(dst, rsa, args.lda, m0, args.a_ext, kbeg + st * BK, args.ka, wid, lane);
-      dma_tile<BKC, CF::BN, CF::NW>(dst + CF::A_BYTES, rsb, args.ldb, n0, args.b_ext, kbeg + st * BK, args.kb, wid, lane);
+      sta.stage(dst, st);
+      stb.stage(dst + CF::A_BYTES, st);
     }
   }
   if constexpr (CF::STAGES == 3) {
@@ -180,9 +343,8 @@ __global__ __launch_bounds__(CF::NT, 2) void gemm_kernel(const GemmArgs args) {
     const int kn = kt + CF::STAGES - 1;  // tile to issue now
     if (kn < nk) {  // its stage was last read in iteration kt-1: free since that barrier
       char* dst = smem + (kn % CF::STAGES) * CF::STAGE;
-      const int k1 = kbeg + kn * BK;
-      dma_tile<AK, CF::BM, CF::NW>(dst, rsa, args.lda, m0, args.a_ext, k1, args.ka, wid, lane);
-      dma_tile<BKC, CF::BN, CF::NW>(dst + CF::A_BYTES, rsb, args.ldb, n0, args.b_ext, k1, args.kb, wid, lane);
+      sta.stage(dst, kn);
+      stb.stage(dst + CF::A_BYTES, kn);
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -210,86 +372,411 @@ __global__ __launch_bounds__(CF::NT, 2) void gemm_kernel(const GemmArgs args) {
     __builtin_amdgcn_s_barrier();
   }
 
-  if constexpr (OUTF32) {
-    if (args.splits > 1) {
-      // split-K: fp32 atomics into C.  Each wave stages its tile through LDS 32 rows at a time
-      // (row stride WTN+4 floats: conflict-free ds_write_b128), then every atomic
-      // wave-instruction adds WTN contiguous floats of one row (256 B: the full-rate shape).
-      constexpr int RS = CF::WTN + 4;
-      float* ct = reinterpret_cast<float*>(smem) + wid * 32 * RS;
-      float* C = reinterpret_cast<float*>(args.C);
+  epilogue<CF, EPI, OUTF32>(args, acc, m0, n0, wm, wn, wid, lane, smem);
+}
+
+// ============================================================================================
+// Ping-pong 256x256 kernel ("PP"): the deep-pipelined structure for large tiles.
+//
+// 8 waves (2 x 4), wave tile 128 x 64, BK = 64.  A K-tile is consumed in 4 phases (k-half ks,
+// row-half ih of the wave tile); each phase = {ds_read its fragments, issue 2 LDS-DMA rounds,
+// [counted vmcnt], s_barrier, lgkmcnt(0), 16 MFMAs, s_barrier}.  Wave group wr = 1 runs one
+// barrier behind group 0, so on every SIMD (waves w and w+4 share one) one wave multiplies while
+// the other reads LDS and issues DMA.
+//
+// LDS: 2 K-tile buffers x (A 32 KiB + B 32 KiB) + 16 KiB sink.  An operand image is split in
+// 4 "rounds" of 8 KiB = (half h of the 256 rows/cols, k-half kh); one round = one 1-KiB
+// buffer_load...lds per wave.  k-contiguous operands use [kh][256 rows][64 B] images (chunk ^
+// ((row >> 1) & 3): conflict-free ds_read_b128), m/n-contiguous operands the [h][64 k][256 B]
+// half-images of the T128/T256 kernels (ds_read_b64_tr_b16).
+//
+// Schedule in window W (tile W's 4 phases, buffer W & 1):
+//   p0: K0 rounds of B (tile W+1)   p1: K1 rounds of A (W+1)   p2: K1 rounds of B (W+1)
+//   p3: K0 rounds of A (W+2)        vmcnt(6) at p1 (retires K1 of W) and p3 (K0 of W+1)
+// A round is restaged >= 2 phases after its last read (the stagger lets the partner group's reads
+// of the previous phase still be in flight one phase later), and read one phase after the wait that
+// retired it.  Rounds past the last K-tile go to the sink with an out-of-range offset, so every
+// phase issues exactly 2 DMA instructions and the counted waits stay exact in the tail.
+namespace ppk {
+constexpr int BUF = 65536;
+constexpr int SINK = 2 * BUF;
+constexpr int SMEM = 2 * BUF + 16384;
+
+template <bool KC>
+MG_DEVICE int round_off(int h, int kh) { return KC ? kh * 16384 + h * 8192 : h * 16384 + kh * 8192; }
+
+template <bool KC>
+MG_DEVICE bf16x8 frag(const char* img, int sb, int ks, int lane) {
+  if constexpr (KC) {
+    const int row = sb * 16 + (lane & 15), ch = lane >> 4;
+    return *reinterpret_cast<const bf16x8*>(img + ks * 16384 + row * 64 + ((ch ^ ((row >> 1) & 3)) << 4));
+  } else {
+    return ::frag<false>(img, sb, ks, lane);
+  }
+}
+
+// Per-wave DMA piece of round (h, kh) of one operand: byte offset at K-tile 0 relative to the
+// split's K start (kOOB when its row/col is out of range), and its k position for the per-lane
+// check of a partial last K-tile.
+struct Piece {
+  uint32_t off0;
+  int kpos;
+};
+
+template <bool KC>
+MG_DEVICE Piece make_piece(long ld, int r0, int ext, int h, int kh, int wid, int lane) {
+  Piece p;
+  if constexpr (KC) {
+    const int row = h * 128 + wid * 16 + (lane >> 2);
+    const int ch = (lane & 3) ^ ((row >> 1) & 3);
+    const int gr = r0 + row;
+    p.kpos = kh * 32 + ch * 8;
+    p.off0 = gr < ext ? (uint32_t)(((long)gr * ld + p.kpos) * 2) : kOOB;
+  } else {
+    const int krow = kh * 32 + wid * 4 + (lane >> 4);
+    const int ch = (lane & 15) ^ swz_mn(krow);
+    const int gc = r0 + h * 128 + ch * 8;
+    p.kpos = krow;
+    p.off0 = gc < ext ? (uint32_t)(((long)krow * ld + gc) * 2) : kOOB;
+  }
+  return p;
+}
+
+// One 1-KiB piece.  dst is wave-uniform (SGPR math only); `tail` = this tile is the partial last
+// K-tile (per-lane k check, rare); t >= nk re-loads tile 0 into the sink (never read).
+MG_DEVICE void issue(char* dst, __amdgpu_buffer_rsrc_t rs, const Piece& pc, bool tail, int klim) {
+  uint32_t off = pc.off0;
+  if (tail) off = pc.kpos < klim ? off : kOOB;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)dst, 16, off, 0, 0, 0);
+}
+}  // namespace ppk
+
+template <bool AK, bool BKC, int EPI, bool OUTF32>
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const GemmArgs args) {
+  using CF = Cfg<256, 256, 2, 4>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+
+  const int nblk = args.tiles_m * args.tiles_n * args.splits;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int wgs = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int ntiles = args.tiles_m * args.tiles_n;
+  const int split = wgs / ntiles;
+  const int wg = wgs % ntiles;
+  const int group = GROUP_M * args.tiles_n;
+  const int first_m = (wg / group) * GROUP_M;
+  const int gm = min(args.tiles_m - first_m, GROUP_M);
+  const int m0 = (first_m + (wg % group) % gm) * 256;
+  const int n0 = ((wg % group) / gm) * 256;
+
+  f32x4 acc[8][4];
 #pragma unroll
-      for (int pass = 0; pass < CF::FM / 2; ++pass) {
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int ii = 0; ii < 2; ++ii)
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int kbeg = split * args.kchunk;
+  const int nk = (min(args.K, kbeg + args.kchunk) - kbeg + BK - 1) / BK;
+  const int swid = __builtin_amdgcn_readfirstlane(wid);
+  const uint32_t sta = AK ? BK * 2 : (uint32_t)(BK * args.lda * 2);
+  const uint32_t stb = BKC ? BK * 2 : (uint32_t)(BK * args.ldb * 2);
+  // operand bases at the split's first k; extents from there
+  const uint32_t a_k0 = AK ? (uint32_t)kbeg * 2 : (uint32_t)((long)kbeg * args.lda * 2);
+  const uint32_t b_k0 = BKC ? (uint32_t)kbeg * 2 : (uint32_t)((long)kbeg * args.ldb * 2);
+  const char* abase = reinterpret_cast<const char*>(args.A) + a_k0;
+  const char* bbase = reinterpret_cast<const char*>(args.B) + b_k0;
+  const uint32_t abytes = args.a_bytes > a_k0 ? args.a_bytes - a_k0 : 0u;
+  const uint32_t bbytes = args.b_bytes > b_k0 ? args.b_bytes - b_k0 : 0u;
+  // k limit relative to the split start (ka/kb: reads as zero beyond), and the partial tile
+  const int kla = min(args.ka, kbeg + args.kchunk) - kbeg, klb = min(args.kb, kbeg + args.kchunk) - kbeg;
+  const int tail_t = min(kla, klb) / BK;  // first K-tile needing per-lane k checks (usually none)
+  ppk::Piece pa[2][2], pb[2][2];
 #pragma unroll
-          for (int j = 0; j < CF::FN; ++j)
-            *reinterpret_cast<f32x4*>(ct + (ii * 16 + (lane & 15)) * RS + j * 16 + (lane >> 4) * 4) =
-                acc[pass * 2 + ii][j];
-        __syncthreads();
-        for (int c = lane; c < CF::WTN; c += 64) {
-          const int n = n0 + wn * CF::WTN + c;
-          for (int r = 0; r < 32; ++r) {
-            const int m = m0 + wm * CF::WTM + pass * 32 + r;
-            if (m < args.M && n < args.N) atomicAdd(C + (long)m * args.ldc + n, ct[r * RS + c]);
-          }
-        }
-        __syncthreads();
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      pa[h][kh] = ppk::make_piece<AK>(args.lda, m0, args.a_ext, h, kh, wid, lane);
+      pb[h][kh] = ppk::make_piece<BKC>(args.ldb, n0, args.b_ext, h, kh, wid, lane);
+    }
+  auto dst_of = [&](int t, int opoff, int ro, int slot) -> char* {
+    return t < nk ? smem + (t & 1) * ppk::BUF + opoff + ro + swid * 1024
+                  : smem + ppk::SINK + slot * 8192 + swid * 1024;
+  };
+  // two pieces of one operand, K-tile t, k-half kh (h = 0, 1 -> sink slots 0, 1)
+  auto stage2A = [&](int t, int kh) {
+    const int tt = t < nk ? t : 0;
+    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(abase, abytes, sta, tt);
+    const bool tail = tt >= tail_t;
+    const int klim = kla - tt * BK;
+    ppk::issue(dst_of(t, 0, ppk::round_off<AK>(0, kh), 0), rs, pa[0][kh], tail, klim);
+    ppk::issue(dst_of(t, 0, ppk::round_off<AK>(1, kh), 1), rs, pa[1][kh], tail, klim);
+  };
+  auto stage2B = [&](int t, int kh) {
+    const int tt = t < nk ? t : 0;
+    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(bbase, bbytes, stb, tt);
+    const bool tail = tt >= tail_t;
+    const int klim = klb - tt * BK;
+    ppk::issue(dst_of(t, 32768, ppk::round_off<BKC>(0, kh), 0), rs, pb[0][kh], tail, klim);
+    ppk::issue(dst_of(t, 32768, ppk::round_off<BKC>(1, kh), 1), rs, pb[1][kh], tail, klim);
+  };
+  // prologue: tile 0 (K0 then K1), then tile 1's K0 rounds of A (window -1, phase 3)
+  stage2A(0, 0); stage2B(0, 0);
+  stage2A(0, 1); stage2B(0, 1);
+  stage2A(1, 0);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs one barrier behind
+  asm volatile("" ::: "memory");
+
+  bf16x8 fa[4], fb[4];
+#ifdef MG_GEMM_STAMPS
+  unsigned long long st[4][6];
+#define PP_STAMP(p, k) if (W == MG_GEMM_STAMPS) st[p][k] = __builtin_amdgcn_s_memtime()
+#else
+#define PP_STAMP(p, k)
+#endif
+  for (int W = 0; W < nk; ++W) {
+    const char* sa = smem + (W & 1) * ppk::BUF;
+    const char* sbb = sa + 32768;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int ks = p >> 1, ih = p & 1;
+      PP_STAMP(p, 0);
+#ifndef MG_PP_NOREAD
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = ppk::frag<AK>(sa, wr * 8 + ih * 4 + i, ks, lane);
+      if (ih == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = ppk::frag<BKC>(sbb, wc * 4 + j, ks, lane);
       }
-      return;
+#else
+      if (W == 0 && p == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { fa[i] = ppk::frag<AK>(sa, wr * 8 + i, 0, lane); fb[i] = ppk::frag<BKC>(sbb, wc * 4 + i, 0, lane); }
+      }
+#endif
+#ifndef MG_PP_NODMA
+      if (p == 0) stage2B(W + 1, 0);
+      if (p == 1) stage2A(W + 1, 1);
+      if (p == 2) stage2B(W + 1, 1);
+      if (p == 3) stage2A(W + 2, 0);
+#endif
+      PP_STAMP(p, 1);
+#ifndef MG_PP_NODMA
+      if (p == 1 || p == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+      PP_STAMP(p, 2);
+      __builtin_amdgcn_s_barrier();
+      PP_STAMP(p, 3);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      PP_STAMP(p, 4);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[ih * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[ih * 4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      PP_STAMP(p, 5);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
     }
   }
-  // ---- epilogue: lane holds C[m][n..n+3]
-  const int nlim = (EPI == 0 && !OUTF32) ? (int)args.ldc : args.N;
+#ifdef MG_GEMM_STAMPS
+  if (args.dbg && lane == 0 && nk > MG_GEMM_STAMPS)
+    for (int p = 0; p < 4; ++p)
+      for (int k = 0; k < 6; ++k) args.dbg[((long)blockIdx.x * 8 + wid) * 24 + p * 6 + k] = st[p][k];
+#endif
+#undef PP_STAMP
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // sink DMA of the tail
+  __syncthreads();
+  epilogue<CF, EPI, OUTF32>(args, acc, m0, n0, wr, wc, wid, lane, smem);
+}
+
+// Split-K for the fp32-accumulate (weight-gradient) layout: pick the split that minimises
+// rounds x per-block work, where rounds = ceil(blocks / concurrent slots) and per-block work =
+// its K-tiles + ~2 tiles of prologue/epilogue (the atomic write-back).  A naive "fill the chip"
+// split leaves a mostly idle second round (e.g. 144 tiles x 4 = 576 blocks on 512 slots).
+static int choose_split(int tiles, int slots, int nkt, int ovh) {
+  int best = 1;
+  long bc = -1;
+  const int maxsp = std::max(1, std::min(32, nkt / 4));
+  for (int sp = 1; sp <= maxsp; ++sp) {
+    const long rounds = ((long)tiles * sp + slots - 1) / slots;
+    const long c = rounds * (cdiv(nkt, sp) + ovh);
+    if (bc < 0 || c * 20 < bc * 19) {  // a further split must save >= 5%
+      bc = c;
+      best = sp;
+    }
+  }
+  return best;
+}
+
+// ovh: per-block prologue + atomic write-back in K-tile units (grows with the tile area)
+static void set_split(GemmArgs& a, int slots, int ovh) {
+  const int nkt = cdiv(a.K, BK);
+  const int sp = choose_split(a.tiles_m * a.tiles_n, slots, nkt, ovh);
+  a.kchunk = cdiv(nkt, sp) * BK;
+  a.splits = cdiv(a.K, a.kchunk);
+}
+
+template <bool AK, bool BKC, int EPI, bool OUTF32>
+void launch_pp(GemmArgs a, hipStream_t stream) {
+  a.tiles_m = cdiv(a.M, 256);
+  a.tiles_n = cdiv(a.N, 256);
+  a.splits = 1;
+  a.kchunk = cdiv(a.K, BK) * BK;
+  if (OUTF32) set_split(a, 256, 6);
+  const int grid = a.tiles_m * a.tiles_n * a.splits;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)gemm_pp_kernel<AK, BKC, EPI, OUTF32>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, ppk::SMEM);
+    attr_set = true;
+  }
+  gemm_pp_kernel<AK, BKC, EPI, OUTF32><<<grid, 512, ppk::SMEM, stream>>>(a);
+}
+
+// ============================================================================================
+// 4-wave 256x256 kernel ("W4"): one wave per SIMD, 128x128 wave tile (256 accumulator registers,
+// 512-register budget), the structure that keeps MFMA busy without a partner wave.
+//
+// Per K-tile kt (BK = 64 = two k32 steps, LDS buffer kt & 1, the T256 images):
+//   phase A: 64 MFMAs on the k32 step 0 fragments while the step-1 fragments are read
+//   s_waitcnt vmcnt(0) lgkmcnt(0) + barrier   (tile kt+1 has landed; buffer kt & 1 fully read)
+//   phase B: LDS-DMA of tile kt+2 into buffer kt & 1, step-0 fragments of tile kt+1 read, 64 MFMAs
+//            on the step-1 fragments
+// One barrier per K-tile; each tile's DMA has ~1.5 K-tiles of MFMA work to land in.
+// MFMA with the accumulator pinned to AGPRs ("+a"): with 256 accumulator registers the compiler's
+// own allocation shuffles them between AGPRs and VGPRs every K-step.  volatile + "memory" keeps
+// program order between the MFMAs and the LDS reads / DMA pieces placed between them: one wave per
+// SIMD issues in order, so a burst of loads would stall its own MFMA stream.
+MG_DEVICE void mfma_acc(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b) : "memory");
+}
+
+namespace w4k {
+constexpr int STAGE = 65536;          // one K-tile: A 32 KiB + B 32 KiB (T256 images)
+constexpr int SINK = 2 * STAGE;       // DMA past the last K-tile lands here (never read)
+constexpr int SMEM = 2 * STAGE + 32768;
+}  // namespace w4k
+
+template <bool AK, bool BKC, int EPI, bool OUTF32>
+__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
+  using CF = Cfg<256, 256, 2, 2>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  const int nblk = args.tiles_m * args.tiles_n * args.splits;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int wgs = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int ntiles = args.tiles_m * args.tiles_n;
+  const int split = wgs / ntiles;
+  const int wg = wgs % ntiles;
+  const int group = GROUP_M * args.tiles_n;
+  const int first_m = (wg / group) * GROUP_M;
+  const int gm = min(args.tiles_m - first_m, GROUP_M);
+  const int m0 = (first_m + (wg % group) % gm) * 256;
+  const int n0 = ((wg % group) / gm) * 256;
+
+  f32x4 acc[8][8];
 #pragma unroll
-  for (int i = 0; i < CF::FM; ++i) {
-    const int m = m0 + wm * CF::WTM + i * 16 + (lane & 15);
-    if (m >= args.M) continue;
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < CF::FN; ++j) {
-      const int n = n0 + wn * CF::WTN + j * 16 + (lane >> 4) * 4;
-      if (n >= nlim) continue;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      const long off = (long)m * args.ldc + n;
-      if constexpr (OUTF32) {
-        float4* cp = reinterpret_cast<float4*>(reinterpret_cast<float*>(args.C) + off);
-        float4 c = *cp;
-        c.x += v[0]; c.y += v[1]; c.z += v[2]; c.w += v[3];
-        *cp = c;
-      } else {
-        if constexpr (EPI == 1 || EPI == 2 || EPI == 3) {
-          if (args.bias) {
-            const uint2 bb = *reinterpret_cast<const uint2*>(args.bias + n);
-            v[0] += bf2f(bb.x & 0xffffu); v[1] += bf2f(bb.x >> 16);
-            v[2] += bf2f(bb.y & 0xffffu); v[3] += bf2f(bb.y >> 16);
-          }
-        }
-        if constexpr (EPI == 2) {
-          *reinterpret_cast<uint2*>(args.aux + off) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int kbeg = split * args.kchunk;
+  const int nk = (min(args.K, kbeg + args.kchunk) - kbeg + BK - 1) / BK;
+  Stager<AK, 256, 4> sta;
+  Stager<BKC, 256, 4> stb;
+  sta.init(args.A, args.a_bytes, args.lda, m0, args.a_ext, kbeg, args.ka, kbeg + args.kchunk, wid, lane);
+  stb.init(args.B, args.b_bytes, args.ldb, n0, args.b_ext, kbeg, args.kb, kbeg + args.kchunk, wid, lane);
+  sta.stage(smem, 0);
+  stb.stage(smem + CF::A_BYTES, 0);
+  if (nk > 1) {
+    sta.stage(smem + w4k::STAGE, 1);
+    stb.stage(smem + w4k::STAGE + CF::A_BYTES, 1);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = gelu_f(v[r]);
-        }
-        if constexpr (EPI == 3) {
-          if (args.thr) {
-            const uint4 rnd = rand4(args.seed, ((uint64_t)m * args.N + n) >> 2);
-            const uint32_t rr[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+  for (int i = 0; i < 8; ++i) fa0[i] = frag<AK>(smem, wm * 8 + i, 0, lane);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = rr[r] >= args.thr ? v[r] * args.scale : 0.f;
-          }
-          const uint2 res = *reinterpret_cast<const uint2*>(args.resid + off);
-          v[0] += bf2f(res.x & 0xffffu); v[1] += bf2f(res.x >> 16);
-          v[2] += bf2f(res.y & 0xffffu); v[3] += bf2f(res.y >> 16);
-        }
-        if constexpr (EPI == 4) {
-          const uint2 pa = *reinterpret_cast<const uint2*>(args.aux + off);
-          v[0] *= gelu_grad(bf2f(pa.x & 0xffffu)); v[1] *= gelu_grad(bf2f(pa.x >> 16));
-          v[2] *= gelu_grad(bf2f(pa.y & 0xffffu)); v[3] *= gelu_grad(bf2f(pa.y >> 16));
-        }
-        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(args.C) + off) =
-            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+  for (int j = 0; j < 8; ++j) fb0[j] = frag<BKC>(smem + CF::A_BYTES, wn * 8 + j, 0, lane);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* sa = smem + (kt & 1) * w4k::STAGE;
+    // phase A: k32 step 0 of tile kt; step-1 fragments read between the MFMAs (one per 2)
+#pragma unroll
+    for (int q = 0; q < 64; ++q) {
+      const int i = q >> 3, j = q & 7;
+      mfma_acc(acc[i][j], fb0[j], fa0[i]);
+      if ((q & 1) == 0 && q < 32) {
+        const int r = q >> 1;  // 0..15: A fragments then B fragments
+        if (r < 8) fa1[r] = frag<AK>(sa, wm * 8 + r, 1, lane);
+        else fb1[r - 8] = frag<BKC>(sa + CF::A_BYTES, wn * 8 + r - 8, 1, lane);
+      }
+    }
+    // tile kt+1 landed (this wave's DMA), every wave done reading buffer kt & 1
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // phase B: k32 step 1 of tile kt; DMA of tile kt+2 into buffer kt & 1 (or the sink) and the
+    // step-0 fragments of tile kt+1 between the MFMAs
+    const int t2 = kt + 2;
+    const int tt = t2 < nk ? t2 : 0;
+    char* dst = t2 < nk ? smem + (kt & 1) * w4k::STAGE : smem + w4k::SINK;
+    const __amdgpu_buffer_rsrc_t ra = sta.rsrc(tt), rb = stb.rsrc(tt);
+    const char* sn = smem + ((kt + 1) & 1) * w4k::STAGE;
+#pragma unroll
+    for (int q = 0; q < 64; ++q) {
+      const int i = q >> 3, j = q & 7;
+      mfma_acc(acc[i][j], fb1[j], fa1[i]);
+      if (q < 32 && (q & 1) == 0) {
+        const int r = q >> 1;  // 16 DMA pieces: 8 of A, 8 of B
+        if (r < 8) sta.piece(dst, ra, tt, r);
+        else stb.piece(t2 < nk ? dst + CF::A_BYTES : dst, rb, tt, r - 8);
+      }
+      if (q >= 32 && (q & 1) == 0) {
+        const int r = (q - 32) >> 1;  // 16 fragment reads of tile kt+1 step 0
+        if (r < 8) fa0[r] = frag<AK>(sn, wm * 8 + r, 0, lane);
+        else fb0[r - 8] = frag<BKC>(sn + CF::A_BYTES, wn * 8 + r - 8, 0, lane);
       }
     }
   }
+  asm volatile("s_nop 15\n s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // MFMA results -> readers
+  __syncthreads();
+  epilogue<CF, EPI, OUTF32>(args, acc, m0, n0, wm, wn, wid, lane, smem);
+}
+
+template <bool AK, bool BKC, int EPI, bool OUTF32>
+void launch_w4(GemmArgs a, hipStream_t stream) {
+  a.tiles_m = cdiv(a.M, 256);
+  a.tiles_n = cdiv(a.N, 256);
+  a.splits = 1;
+  a.kchunk = cdiv(a.K, BK) * BK;
+  if (OUTF32) set_split(a, 256, 6);
+  const int grid = a.tiles_m * a.tiles_n * a.splits;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)gemm_w4_kernel<AK, BKC, EPI, OUTF32>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, w4k::SMEM);
+    attr_set = true;
+  }
+  gemm_w4_kernel<AK, BKC, EPI, OUTF32><<<grid, 256, w4k::SMEM, stream>>>(a);
 }
 
 template <class CF, bool AK, bool BKC, int EPI, bool OUTF32>
@@ -298,15 +785,7 @@ void launch(GemmArgs a, hipStream_t stream) {
   a.tiles_n = cdiv(a.N, CF::BN);
   a.splits = 1;
   a.kchunk = cdiv(a.K, BK) * BK;
-  if (OUTF32) {  // weight gradient: small outputs, huge K -> split K until the chip is full
-    const int tiles = a.tiles_m * a.tiles_n;
-    const int slots = 256 * (CF::SMEM <= 80 * 1024 ? 2 : 1);
-    int sp = tiles >= (3 * slots) / 4 ? 1 : std::min(16, cdiv(slots, tiles));
-    const int nkt = cdiv(a.K, BK);
-    sp = std::min(sp, nkt);
-    a.kchunk = cdiv(nkt, sp) * BK;
-    a.splits = cdiv(a.K, a.kchunk);
-  }
+  if (OUTF32) set_split(a, 256 * (CF::SMEM <= 80 * 1024 ? 2 : 1), 2 + CF::BM * CF::BN / 16384);
   const int grid = a.tiles_m * a.tiles_n * a.splits;
   static bool attr_set = false;
   if (!attr_set) {
@@ -317,22 +796,30 @@ void launch(GemmArgs a, hipStream_t stream) {
   gemm_kernel<CF, AK, BKC, EPI, OUTF32><<<grid, CF::NT, CF::SMEM, stream>>>(a);
 }
 
-// Tile config per shape (measured, bench/bench_gemm.py): the 256x256 tile (1 workgroup/CU, more
-// MFMA work per LDS byte) wins once it has >= 2 full rounds of tiles on the 256 CUs (LM head:
-// 1.57 vs 1.87 ms); otherwise 128x128 (2 workgroups/CU, finer quantisation) is as fast or faster,
-// and always for the split-K weight gradient.
-int pick_config(int M, int N, bool outf32) {
+// Tile config per shape and layout, from bench/bench_gemm.py at the GPT-2 step shapes (M = 32768
+// tokens) and the 4096^3 / 8192^3 squares (profiles/round1_gemm_bench.jsonl):
+//   forward (NT):  W4 (1 wave/SIMD, 128x128 wave tiles) once there are >= 3 rounds of 256^2 tiles
+//                  or a long K; T128 for the small N = 768, K = 768 projection
+//   dgrad (NN), wgrad (TN): the ping-pong 256^2 kernel (PP) for long K or many tiles / large
+//                  weight-gradient outputs; T128 for 768 x 768
+// 256-tile kernels lose to T128 when a short K leaves prologue/epilogue dominant or when the tile
+// count quantises badly onto the 256 CUs.
+int pick_config(int M, int N, int K, int layout) {
   if (g_variant) return g_variant;
-  if (outf32) return 1;
   const long t256 = (long)cdiv(M, 256) * cdiv(N, 256);
-  return t256 >= 512 ? 2 : 1;
+  if (layout == 0) return (t256 >= 768 || (t256 >= 384 && K >= 2048)) ? 5 : 1;
+  if (layout == 1) return (K >= 1536 || t256 >= 1024) ? 4 : 1;
+  return (long)M * N >= (1L << 20) ? 4 : 1;
 }
 
 template <bool AK, bool BKC, int EPI, bool OUTF32>
 void dispatch(const GemmArgs& a, hipStream_t stream) {
-  switch (pick_config(a.M, a.N, OUTF32)) {
+  const int layout = OUTF32 ? 2 : (BKC ? 0 : 1);
+  switch (pick_config(a.M, a.N, a.K, layout)) {
     case 2: launch<T256, AK, BKC, EPI, OUTF32>(a, stream); break;
     case 3: launch<T2x1, AK, BKC, EPI, OUTF32>(a, stream); break;
+    case 4: launch_pp<AK, BKC, EPI, OUTF32>(a, stream); break;
+    case 5: launch_w4<AK, BKC, EPI, OUTF32>(a, stream); break;
     default: launch<T128, AK, BKC, EPI, OUTF32>(a, stream); break;
   }
 }
@@ -342,6 +829,7 @@ void dispatch(const GemmArgs& a, hipStream_t stream) {
 namespace mg {
 
 void gemm_set_variant(int v) { g_variant = v; }
+void gemm_set_debug_buffer(unsigned long long* p) { g_dbg = p; }
 int gemm_get_variant() { return g_variant; }
 
 // layout: 0 = NT (fwd), 1 = NN (dgrad), 2 = TN (wgrad, fp32 accumulate into C)
@@ -355,10 +843,11 @@ void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long l
   a.A = A; a.B = B; a.C = C; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.M = M; a.N = N; a.K = K; a.a_ext = a_ext; a.b_ext = b_ext; a.ka = ka; a.kb = kb;
   a.bias = bias; a.aux = aux; a.resid = resid; a.seed = seed;
-  a.thr = p > 0.f ? dropout_threshold(p) : 0u;
-  a.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  a.thr = dropout_threshold8(p);  // EPI 3 residual dropout: 8-bit row-block mask (common.h)
+  a.scale = dropout_scale8(a.thr);
   a.tiles_m = a.tiles_n = a.splits = 1;
   a.kchunk = K;
+  a.dbg = g_dbg;
   if (layout == 0) {
     if (epi == 0) dispatch<true, true, 0, false>(a, stream);
     else if (epi == 1) dispatch<true, true, 1, false>(a, stream);

@@ -9,7 +9,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.fixture(autouse=True, params=[0, 1, 2, 3], ids=["auto", "t128", "t256", "t256x128"])
+@pytest.fixture(autouse=True, params=[0, 1, 2, 3, 4, 5], ids=["auto", "t128", "t256", "t256x128", "pp256", "w4"])
 def tile_config(request):
     """Run every GEMM test under each tile configuration of gemm.hip (0 = per-shape choice)."""
     from mingpt_distributed_amd.ops._ext import ext

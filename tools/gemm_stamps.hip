@@ -1,0 +1,75 @@
+// gemm_stamps: diagnostic build of the GEMM kernels with per-phase s_memtime stamps.
+// Runs one M x N x K NT GEMM (random bf16) under a forced tile config and prints, per phase of
+// the ping-pong kernel's K-tile MG_GEMM_STAMPS, the median cycles of each segment over all waves:
+//   reads+DMA issue | vmcnt wait | barrier 1 | lgkmcnt wait | MFMA | barrier 2 (next phase start)
+// Build: hipcc --offload-arch=gfx950 -O3 -DMG_GEMM_STAMPS=20 -Icsrc/include tools/gemm_stamps.hip
+#include "../csrc/kernels/gemm.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+int main(int argc, char** argv) {
+  const int M = argc > 1 ? atoi(argv[1]) : 8192, N = argc > 2 ? atoi(argv[2]) : 8192,
+            K = argc > 3 ? atoi(argv[3]) : 8192, variant = argc > 4 ? atoi(argv[4]) : 4;
+  std::vector<uint16_t> ha((size_t)M * K), hb((size_t)N * K);
+  std::mt19937 rng(1);
+  std::uniform_int_distribution<int> d(0, 0x7f);
+  for (auto& v : ha) v = 0x3f00 | d(rng);  // bf16 in [0.5, 1): random mantissas
+  for (auto& v : hb) v = 0xbf00 | d(rng);
+  bf16_t *a, *b, *c;
+  unsigned long long* dbg;
+  hipMalloc(&a, ha.size() * 2);
+  hipMalloc(&b, hb.size() * 2);
+  hipMalloc(&c, (size_t)M * N * 2);
+  const int blocks = cdiv(M, 256) * cdiv(N, 256);
+  hipMalloc(&dbg, (size_t)blocks * 8 * 24 * 8);
+  hipMemset(dbg, 0, (size_t)blocks * 8 * 24 * 8);
+  hipMemcpy(a, ha.data(), ha.size() * 2, hipMemcpyHostToDevice);
+  hipMemcpy(b, hb.data(), hb.size() * 2, hipMemcpyHostToDevice);
+  mg::gemm_set_variant(variant);
+  auto run = [&] {
+    mg::gemm(0, 0, a, b, c, K, K, N, M, N, K, M, N, K, K, nullptr, nullptr, nullptr, 0.f, 0, 0,
+             (size_t)M * K * 2, (size_t)N * K * 2);
+  };
+  for (int i = 0; i < 3; ++i) run();
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  hipEventRecord(e0);
+  for (int i = 0; i < 5; ++i) run();
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms;
+  hipEventElapsedTime(&ms, e0, e1);
+  printf("variant %d  %dx%dx%d: %.3f ms  %.1f TF/s\n", variant, M, N, K, ms / 5, 2.0 * M * N * K / (ms / 5 * 1e-3) / 1e12);
+  mg::gemm_set_debug_buffer(dbg);
+  run();
+  hipDeviceSynchronize();
+  std::vector<unsigned long long> h((size_t)blocks * 8 * 24);
+  hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost);
+  const char* seg[6] = {"reads+dma", "vmcnt", "barrier1", "lgkmcnt", "mfma", "barrier2"};
+  for (int grp = 0; grp < 2; ++grp) {
+    printf("group %d (waves %d-%d), median cycles per segment:\n", grp, grp * 4, grp * 4 + 3);
+    for (int p = 0; p < 4; ++p) {
+      printf("  phase %d:", p);
+      for (int k = 0; k < 6; ++k) {
+        std::vector<long long> v;
+        for (int bl = 0; bl < blocks; ++bl)
+          for (int w = grp * 4; w < grp * 4 + 4; ++w) {
+            const unsigned long long* s = &h[((size_t)bl * 8 + w) * 24];
+            const unsigned long long t0 = s[p * 6 + k];
+            const unsigned long long t1 = k < 5 ? s[p * 6 + k + 1] : (p < 3 ? s[(p + 1) * 6] : 0);
+            if (t0 && t1) v.push_back((long long)(t1 - t0));
+          }
+        if (v.empty()) { printf(" %s=-", seg[k]); continue; }
+        std::sort(v.begin(), v.end());
+        printf(" %s=%lld", seg[k], v[v.size() / 2]);
+      }
+      printf("\n");
+    }
+  }
+  return 0;
+}
