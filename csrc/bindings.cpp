@@ -362,6 +362,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_dropout_residual", &bias_dropout_residual);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("dropout_bwd", &dropout_bwd);
+  m.def("attention_set_bwd_variant", &mg::attention_set_bwd_variant);
   m.def("bias_grad", &bias_grad);
   m.def("dropout_bias_grad", &dropout_bias_grad);
   m.def("gemm", &gemm);

@@ -63,6 +63,7 @@ int gemm_get_variant();
 // attention.hip -- causal flash attention, hd <= 64; qkv [B*T, 3D], out [B*T, D], lse [B*H*T]
 // dmask: dropout keep-bits written by fwd when p > 0 (attention_dropout_mask_words u32), read by bwd
 size_t attention_dropout_mask_words(int B, int T, int H);
+void attention_set_bwd_variant(int v);  // 0 auto (256-key blocks), 1 force 128-key blocks
 void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, uint32_t* dmask, int B, int T, int H,
                    int hd, float p, uint64_t seed, hipStream_t stream);
 // delta [B*H*T] and dq [B*T*D] fp32 are workspaces; writes all three slots of dqkv

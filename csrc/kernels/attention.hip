@@ -61,11 +61,23 @@ struct AttnArgs {
   int B, T, H, hd, D;
   float scale_log2;    // log2(e) / sqrt(hd)
   uint64_t seed;
+  uint32_t seed_key;   // fwd dropout hash key derived from seed
   uint32_t thr;        // 8-bit keep threshold: keep iff random byte >= thr (0 = no dropout)
   float dscale;        // 1 / (1 - thr/256)
 };
 
 MG_DEVICE float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }  // v_exp_f32, no denorm fixup
+
+// 32-bit avalanche mixer (xorshift-multiply, "lowbias32" constants): a bijection with good
+// avalanche, 5 VALU ops; the attention-dropout bytes are mix32 of distinct counters.
+MG_DEVICE uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
 
 MG_DEVICE bf16x8 lds_row_frag(const char* base, int row, int ch) {
   return *reinterpret_cast<const bf16x8*>(base + lds_off(row, ch));
@@ -169,50 +181,61 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
           s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
               lds_row_frag(sk, sub * 32 + l32, ks * 2 + h32), qf[ks], s[sub], 0, 0, 0);
       }
-      // scale + mask, row max
+      // mask only the tiles that need it (diagonal / past T: wave-uniform), row max on raw scores
       const bool diag = k0 + 63 > q0 + 32 * w;
-      float mx = kNegBig;
+      if (diag || k0 + 64 > a.T) {
 #pragma unroll
-      for (int sub = 0; sub < 2; ++sub)
+        for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = k0 + sub * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
-          float v = s[sub][r] * a.scale_log2;
-          if ((diag && key > myq) || key >= a.T) v = kNegBig;
-          s[sub][r] = v;
-          mx = fmaxf(mx, v);
-        }
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + sub * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+            if (key > myq || key >= a.T) s[sub][r] = kNegBig;
+          }
+      }
+      float mx = s[0][0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s[0][r]);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[1][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m, mx);
-      const float alpha = fexp2(m - mn);
-      m = mn;
+      // online softmax; the O / l rescale runs only when some lane's max grew (exact: lanes whose
+      // max did not grow get alpha = 1), which after the first few tiles is rare
+      if (__any(mx > m)) {
+        const float mn = fmaxf(m, mx);
+        const float alpha = fexp2((m - mn) * a.scale_log2);
+        m = mn;
+        l *= alpha;
+        o0 *= alpha;
+        o1 *= alpha;
+      }
+      // p = exp2(s * c - m * c): the softmax scale folded into one FMA per element
+      const float mc = m * a.scale_log2;
       float rs = 0.f;
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = fexp2(s[sub][r] - mn);
+          const float p = fexp2(__builtin_fmaf(s[sub][r], a.scale_log2, -mc));
           s[sub][r] = p;
           rs += p;
         }
       rs += __shfl_xor(rs, 32, 64);
-      l = l * alpha + rs;
-      o0 *= alpha;
-      o1 *= alpha;
+      l += rs;
       if (a.thr) {  // attention dropout on P (for O only; l uses the undropped P)
-        // one Philox call = 16 random bytes = this lane's 16 elements of a 32-key subtile;
-        // keep iff byte >= thr (8-bit threshold).  The keep bits are stored for the backward.
+        // 32 random bytes per lane and tile from a counter hash (the keep bits are stored for the
+        // backward, so this generator never has to be replayed elsewhere); keep iff byte >= thr.
+        // The keep scale 1/(1-p) is applied once to O at the end.
+        const uint64_t ctr = (drop_row * (uint64_t)ntiles_all + t) * 2 + h32;
+        const uint32_t base = mix32((uint32_t)ctr ^ mix32((uint32_t)(ctr >> 32) ^ a.seed_key));
+        uint32_t rw[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) rw[i] = mix32(base + (uint32_t)i * 0x9E3779B9u);
         uint32_t bits = 0;
 #pragma unroll
-        for (int sub = 0; sub < 2; ++sub) {
-          const uint4 rnd = rand4(a.seed, ((drop_row * (uint64_t)ntiles_all + t) * 2 + h32) * 2 + sub);
-          const uint32_t rr[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const bool keep = ((rr[r >> 2] >> (8 * (r & 3))) & 0xffu) >= a.thr;
-            s[sub][r] = keep ? s[sub][r] * a.dscale : 0.f;
-            bits |= (uint32_t)keep << (sub * 16 + r);
-          }
+        for (int idx = 31; idx >= 0; --idx) {  // shift-in: element idx ends at bit idx
+          const bool keep = ((rw[idx >> 2] >> (8 * (idx & 3))) & 0xffu) >= a.thr;
+          s[idx >> 4][idx & 15] = keep ? s[idx >> 4][idx & 15] : 0.f;
+          bits = (bits << 1) | (uint32_t)keep;
         }
         if (myq < a.T) a.dmask[(long)drop_row * (2 * ntiles_all) + t * 2 + h32] = bits;
       }
@@ -237,8 +260,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
   }
 
   if (myq < a.T) {
-    const float inv = 1.f / l;
-    if (h32 == 0) a.lse[(long)bh * a.T + myq] = m + log2f(l);
+    const float inv = (a.thr ? a.dscale : 1.f) / l;
+    if (h32 == 0) a.lse[(long)bh * a.T + myq] = m * a.scale_log2 + log2f(l);  // log2 domain
     bf16_t* orow = a.out + ((long)b * a.T + myq) * a.D + hh * a.hd;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -490,6 +513,271 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const AttnArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------- backward, 256 keys
+// Same algorithm, 8 waves = 256 keys per workgroup (1 workgroup / CU, 2 waves / SIMD): dQ of a
+// query row is summed over T/256 instead of T/128 key blocks, halving the fp32 atomic bytes, which
+// at ~1.3 TB/s chip-wide are this pass's floor (MI355X_MICROARCH 'Global float atomics').  The two
+// waves that split a 32x32 dQ tile's 256 keys add their partials through LDS first.
+// Per-element math: S accumulators start at -lse/c (p = exp2(c * S)), lse/delta/keep-words are read
+// 4 rows per ds_read_b128, the causal mask runs only on diagonal tiles.
+constexpr int KB2 = 256;
+constexpr int B2_Q = 0;
+constexpr int B2_DO = B2_Q + BQ * ROWB;             // 8 KiB
+constexpr int B2_K = B2_DO + BQ * ROWB;             // 16 KiB
+constexpr int B2_DS = B2_K + KB2 * ROWB;            // 48 KiB
+constexpr int B2_L = B2_DS + KB2 * ROWB;            // 80 KiB: lse/c [64], delta [64] f32
+constexpr int B2_MW = B2_L + 2 * BQ * 4;            // keep-words [8 cols][64 q] u32
+constexpr int B2_P = B2_MW + 8 * BQ * 4;            // dQ partials [4 tiles][4][64 lanes][4] f32
+constexpr int B2_SMEM = B2_P + 4 * 4 * 64 * 16;     // 99 KiB
+
+// [rows][64 cols] bf16 tile -> LDS image (lds_off swizzle), NT threads, rows multiple of NT/8
+template <int ROWS, int NT>
+MG_DEVICE void load_rows(uint4 (&reg)[ROWS * 8 / NT], const bf16_t* base, long ld, int r0, int rows, int hd) {
+#pragma unroll
+  for (int i = 0; i < ROWS * 8 / NT; ++i) {
+    const int idx = threadIdx.x + NT * i;
+    const int row = idx >> 3, ch = idx & 7;
+    const int r = r0 + row;
+    reg[i] = (r < rows && ch * 8 < hd) ? ld16(base + (long)r * ld + ch * 8) : make_uint4(0, 0, 0, 0);
+  }
+}
+template <int ROWS, int NT>
+MG_DEVICE void store_rows(char* lds, const uint4 (&reg)[ROWS * 8 / NT]) {
+#pragma unroll
+  for (int i = 0; i < ROWS * 8 / NT; ++i) {
+    const int idx = threadIdx.x + NT * i;
+    *reinterpret_cast<uint4*>(lds + lds_off(idx >> 3, idx & 7)) = reg[i];
+  }
+}
+
+template <int NKS>
+__global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int w = threadIdx.x >> 6;
+  const int bh = blockIdx.x % (a.B * a.H);
+  const int kb = blockIdx.x / (a.B * a.H);  // key block 0 (sweeps every query) first
+  const int b = bh / a.H, hh = bh % a.H;
+  const int kb0 = kb * KB2;
+  const long ld = 3L * a.D;
+  const bf16_t* Qg = a.qkv + (long)b * a.T * ld + hh * a.hd;
+  const bf16_t* Kg = Qg + a.D;
+  const bf16_t* Vg = Qg + 2 * a.D;
+  const bf16_t* dOg = a.dout + (long)b * a.T * a.D + hh * a.hd;
+  const float* lseg = a.lse + (long)bh * a.T;
+  const float* dlg = a.delta + (long)bh * a.T;
+  char* sK = smem + B2_K;
+  char* sdS = smem + B2_DS;
+  const float* sL = reinterpret_cast<const float*>(smem + B2_L);
+  const uint32_t* sMW = reinterpret_cast<const uint32_t*>(smem + B2_MW);
+  const float inv_c = 1.f / a.scale_log2;
+
+  int mykey, wave_kmin;
+  bf16x8 vf[4];
+  {
+    const int lane = threadIdx.x & 63, h32 = lane >> 5, l32 = lane & 31;
+    mykey = kb0 + 32 * w + l32;
+    wave_kmin = kb0 + 32 * w;
+    uint4 rk[4];
+    load_rows<KB2, 512>(rk, Kg, ld, kb0, a.T, a.hd);
+    store_rows<KB2, 512>(sK, rk);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int d = ks * 16 + 8 * h32;
+      const bool ok = mykey < a.T && d < a.hd;
+      vf[ks] = __builtin_bit_cast(bf16x8, ok ? ld16(Vg + (long)mykey * ld + d) : make_uint4(0, 0, 0, 0));
+    }
+  }
+  // this lane's dropout bit inside the forward's keep-words (see attn_fwd_kernel)
+  const int mw_col = (w >> 1) * 2 + ((mykey >> 2) & 1);
+  const int mw_bit = ((mykey & 32) >> 1) | (mykey & 3) | (((mykey >> 3) & 3) << 2);
+  const int ntw = 2 * ((a.T + 63) / 64);
+  const int t0w = (kb0 / 64) * 2;
+
+  f32x16 dk0 = {0}, dk1 = {0}, dv0 = {0}, dv1 = {0};
+  const int qt0 = kb0 / BQ;
+  const int nqt = (a.T + BQ - 1) / BQ;
+
+  uint4 rq[1], rd[1];
+  float rl = 0.f;
+  uint32_t rmw = 0;
+  auto issue = [&](int qt) {
+    load_rows<BQ, 512>(rq, Qg, ld, qt * BQ, a.T, a.hd);
+    load_rows<BQ, 512>(rd, dOg, a.D, qt * BQ, a.T, a.hd);
+    const int t = threadIdx.x;
+    if (t < 2 * BQ) {
+      const int q = qt * BQ + (t & (BQ - 1));
+      rl = q < a.T ? (t < BQ ? lseg[q] * inv_c : dlg[q]) : 0.f;
+    }
+    if (a.thr) {  // word j of query row q -> sMW[j * 64 + q]
+      const int q = qt * BQ + (t & 63), j = t >> 6;
+      rmw = (q < a.T && t0w + j < ntw) ? a.dmask[((long)bh * a.T + q) * ntw + t0w + j] : 0u;
+    }
+  };
+  auto commit = [&]() {
+    store_rows<BQ, 512>(smem + B2_Q, rq);
+    store_rows<BQ, 512>(smem + B2_DO, rd);
+    if (threadIdx.x < 2 * BQ) reinterpret_cast<float*>(smem + B2_L)[threadIdx.x] = rl;
+    if (a.thr) reinterpret_cast<uint32_t*>(smem + B2_MW)[threadIdx.x] = rmw;
+  };
+  issue(qt0);
+  commit();
+  __syncthreads();
+
+  for (int qt = qt0; qt < nqt; ++qt) {
+    const char* sQ = smem + B2_Q;
+    const char* sdO = smem + B2_DO;
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
+    const int h32 = lane >> 5, l32 = lane & 31;
+    const bool more = qt + 1 < nqt;
+    if (more) issue(qt + 1);
+    const int qbase = qt * BQ;
+    char* myds = sdS + w * 32 * ROWB;
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      const int qsub0 = qbase + qs * 32;
+      if (qsub0 + 31 < wave_kmin || wave_kmin >= a.T) {  // every query precedes every key: dS = 0
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int qc = qs * 32 + 8 * g + 4 * h32;
+          *reinterpret_cast<uint2*>(myds + lds_off(l32, qc >> 3) + (qc & 7) * 2) = make_uint2(0, 0);
+        }
+        continue;
+      }
+      // row constants of this lane's 16 rows (4 consecutive rows per float4)
+      float lr[16], dl[16];
+      uint32_t mwr[16];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int q4 = qs * 32 + 8 * g + 4 * h32;
+        const float4 x = *reinterpret_cast<const float4*>(sL + q4);
+        const float4 y = *reinterpret_cast<const float4*>(sL + BQ + q4);
+        lr[4 * g] = -x.x; lr[4 * g + 1] = -x.y; lr[4 * g + 2] = -x.z; lr[4 * g + 3] = -x.w;
+        dl[4 * g] = y.x; dl[4 * g + 1] = y.y; dl[4 * g + 2] = y.z; dl[4 * g + 3] = y.w;
+        if (a.thr) {
+          const uint4 m4 = *reinterpret_cast<const uint4*>(sMW + mw_col * 64 + q4);
+          mwr[4 * g] = m4.x; mwr[4 * g + 1] = m4.y; mwr[4 * g + 2] = m4.z; mwr[4 * g + 3] = m4.w;
+        }
+      }
+      f32x16 s, dp = {0};
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] = lr[r];  // S' = Q K^T - lse/c
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_frag(sQ, qs * 32 + l32, ks * 2 + h32),
+                                                    lds_row_frag(sK, 32 * w + l32, ks * 2 + h32), s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_frag(sdO, qs * 32 + l32, ks * 2 + h32), vf[ks], dp, 0, 0, 0);
+      }
+      // rows = queries qs*32 + (r&3) + 8(r>>2) + 4*h32 ; col = key (lane).  In place:
+      // s <- dropped P (dV operand), dp <- dS = P * (dP~ * Z - delta).
+      const bool needmask = wave_kmin + 31 > qsub0 || qsub0 + 31 >= a.T;  // wave-uniform
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p = fexp2(s[r] * a.scale_log2);
+        if (needmask) {
+          const int q = qsub0 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+          if (mykey > q || q >= a.T) p = 0.f;
+        }
+        float dpv = dp[r], pdrop = p;
+        if (a.thr) {
+          const float z = (mwr[r] >> mw_bit) & 1u ? a.dscale : 0.f;
+          pdrop = p * z;
+          dpv *= z;
+        }
+        s[r] = pdrop;
+        dp[r] = p * (dpv - dl[r]);
+      }
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const bf16x8 pf = pack_frag(s, st);
+        const bf16x8 dsf = pack_frag(dp, st);
+        const int r0 = qs * 32 + 16 * st + 4 * h32;
+        const int cb = 16 * ((lane >> 4) & 1);
+        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sdO, r0, r0 + 8, cb, lane), pf, dv0, 0, 0, 0);
+        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sQ, r0, r0 + 8, cb, lane), dsf, dk0, 0, 0, 0);
+        if constexpr (NKS > 2) {
+          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sdO, r0, r0 + 8, 32 + cb, lane), pf, dv1, 0, 0, 0);
+          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sQ, r0, r0 + 8, 32 + cb, lane), dsf, dk1, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {  // dS^T image row = key, 4 consecutive q per 8-byte write
+        const int qc = qs * 32 + 8 * g + 4 * h32;
+        *reinterpret_cast<uint2*>(myds + lds_off(l32, qc >> 3) + (qc & 7) * 2) =
+            make_uint2(pack2(dp[4 * g], dp[4 * g + 1]), pack2(dp[4 * g + 2], dp[4 * g + 3]));
+      }
+    }
+    __syncthreads();  // dS of all 256 keys in LDS
+    // dQ[64 q][64 d] = dS[64 q][256 keys] K[256 keys][64 d]: 32x32 output tile (qs, dblk) = w & 3,
+    // key half kh = w >> 2; the kh = 1 wave hands its partial to the kh = 0 wave through LDS.
+    const int tile = w & 3, kh = w >> 2;
+    const int qs = tile >> 1, dblk = tile & 1;
+    const bool act1 = dblk * 32 < a.hd && qbase + qs * 32 + 31 >= kb0 + 128 && kb0 + 128 < a.T;
+    const bool act0 = dblk * 32 < a.hd && qbase + qs * 32 + 31 >= kb0;
+    f32x16 dq = {0};
+    if (kh ? act1 : act0) {
+      const int cb = 16 * ((lane >> 4) & 1);
+#pragma unroll 2
+      for (int kk = 0; kk < 8; ++kk) {
+        const int kr0 = kh * 128 + kk * 16 + 8 * h32;
+        const bf16x8 af = lds_tr_frag(sdS, kr0, kr0 + 4, qs * 32 + cb, lane);
+        dq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, lds_tr_frag(sK, kr0, kr0 + 4, dblk * 32 + cb, lane), dq, 0, 0, 0);
+      }
+    }
+    float* part = reinterpret_cast<float*>(smem + B2_P) + tile * 4 * 64 * 4;
+    if (kh == 1 && act1) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f32x4*>(part + (g * 64 + lane) * 4) =
+            f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
+    }
+    __syncthreads();
+    if (kh == 0 && act0) {
+      if (act1) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 x = *reinterpret_cast<const f32x4*>(part + (g * 64 + lane) * 4);
+          dq[4 * g] += x[0]; dq[4 * g + 1] += x[1]; dq[4 * g + 2] += x[2]; dq[4 * g + 3] += x[3];
+        }
+      }
+      const int d = dblk * 32 + l32;
+      if (d < a.hd) {
+        float* dqb = a.dq + ((long)b * a.T) * a.D + hh * a.hd + d;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int q = qbase + qs * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+          if (q < a.T) atomicAdd(dqb + (long)q * a.D, dq[r]);
+        }
+      }
+    }
+    if (more) commit();
+    __syncthreads();
+  }
+
+  const int lane = threadIdx.x & 63, h32 = lane >> 5;
+  if (mykey < a.T) {
+    const float sc = a.scale_log2 * 0.6931471805599453f;  // 1/sqrt(hd)
+    bf16_t* krow = a.dqkv + ((long)b * a.T + mykey) * ld + a.D + hh * a.hd;
+    bf16_t* vrow = krow + a.D;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 8 * g + 4 * h32;
+      if (d < a.hd) {
+        *reinterpret_cast<uint2*>(krow + d) = make_uint2(pack2(dk0[4 * g] * sc, dk0[4 * g + 1] * sc),
+                                                         pack2(dk0[4 * g + 2] * sc, dk0[4 * g + 3] * sc));
+        *reinterpret_cast<uint2*>(vrow + d) = make_uint2(pack2(dv0[4 * g], dv0[4 * g + 1]),
+                                                         pack2(dv0[4 * g + 2], dv0[4 * g + 3]));
+      }
+      if (32 + d < a.hd) {
+        *reinterpret_cast<uint2*>(krow + 32 + d) = make_uint2(pack2(dk1[4 * g] * sc, dk1[4 * g + 1] * sc),
+                                                              pack2(dk1[4 * g + 2] * sc, dk1[4 * g + 3] * sc));
+        *reinterpret_cast<uint2*>(vrow + 32 + d) = make_uint2(pack2(dv1[4 * g], dv1[4 * g + 1]),
+                                                              pack2(dv1[4 * g + 2], dv1[4 * g + 3]));
+      }
+    }
+  }
+}
+
 // dqkv Q slot = bf16(dq * scale)
 __global__ __launch_bounds__(256) void attn_dq_finalize_kernel(const float* __restrict__ dq,
                                                                bf16_t* __restrict__ dqkv, long rows,
@@ -580,11 +868,20 @@ void attention_decode(const bf16_t* qkv_new, bf16_t* cache, bf16_t* out, int B, 
                                                    1.4426950408889634f / sqrtf((float)hd));
 }
 
+static int g_attn_bwd_variant = 0;  // 0 auto (256-key blocks), 1 force 128-key blocks
+
 static AttnArgs make_args(int B, int T, int H, int hd, float p, uint64_t seed) {
   AttnArgs a{};
   a.B = B; a.T = T; a.H = H; a.hd = hd; a.D = H * hd;
   a.scale_log2 = 1.4426950408889634f / sqrtf((float)hd);
   a.seed = seed;
+  {  // host copy of mix32: per-launch key for the forward's dropout hash
+    auto mix = [](uint32_t x) {
+      x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+      return x;
+    };
+    a.seed_key = mix((uint32_t)seed) ^ mix((uint32_t)(seed >> 32) + 0x9E3779B9u);
+  }
   // 8-bit dropout threshold (as FlashAttention does): effective p = thr / 256
   int thr = p > 0.f ? (int)lrintf(p * 256.f) : 0;
   if (p > 0.f) thr = thr < 1 ? 1 : (thr > 255 ? 255 : thr);
@@ -592,6 +889,8 @@ static AttnArgs make_args(int B, int T, int H, int hd, float p, uint64_t seed) {
   a.dscale = thr ? 256.f / (256.f - (float)thr) : 1.f;
   return a;
 }
+
+void attention_set_bwd_variant(int v) { g_attn_bwd_variant = v; }
 
 size_t attention_dropout_mask_words(int B, int T, int H) {
   return (size_t)B * H * T * 2 * ((T + 63) / 64);
@@ -618,10 +917,24 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
   const long nchunks = (long)B * T * H * hd / 8;
   attn_bwd_pre_kernel<<<cdiv(nchunks, 256), 256, 0, stream>>>(dout, out, delta, B, T, H, hd, H * hd);
   hipMemsetAsync(dq, 0, sizeof(float) * (size_t)B * T * H * hd, stream);
-  const int grid = cdiv(T, 128) * B * H;
-  if (hd > 32) attn_bwd_kernel<4><<<grid, 256, BWD_SMEM, stream>>>(a);
-  else if (hd > 16) attn_bwd_kernel<2><<<grid, 256, BWD_SMEM, stream>>>(a);
-  else attn_bwd_kernel<1><<<grid, 256, BWD_SMEM, stream>>>(a);
+  if (g_attn_bwd_variant != 1 && T > 128) {  // 256-key blocks (half the dQ atomics)
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute((const void*)attn_bwd256_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, B2_SMEM);
+      hipFuncSetAttribute((const void*)attn_bwd256_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, B2_SMEM);
+      hipFuncSetAttribute((const void*)attn_bwd256_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, B2_SMEM);
+      attr = true;
+    }
+    const int grid = cdiv(T, KB2) * B * H;
+    if (hd > 32) attn_bwd256_kernel<4><<<grid, 512, B2_SMEM, stream>>>(a);
+    else if (hd > 16) attn_bwd256_kernel<2><<<grid, 512, B2_SMEM, stream>>>(a);
+    else attn_bwd256_kernel<1><<<grid, 512, B2_SMEM, stream>>>(a);
+  } else {
+    const int grid = cdiv(T, 128) * B * H;
+    if (hd > 32) attn_bwd_kernel<4><<<grid, 256, BWD_SMEM, stream>>>(a);
+    else if (hd > 16) attn_bwd_kernel<2><<<grid, 256, BWD_SMEM, stream>>>(a);
+    else attn_bwd_kernel<1><<<grid, 256, BWD_SMEM, stream>>>(a);
+  }
   const long n8 = (long)B * T * (H * hd / 8);
   attn_dq_finalize_kernel<<<cdiv(n8, 256), 256, 0, stream>>>(dq, dqkv, (long)B * T, H * hd,
                                                              1.f / sqrtf((float)hd));

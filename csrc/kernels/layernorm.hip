@@ -99,46 +99,64 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       if (c >= D) wf[i][j] = 0.f;
     }
   }
-  for (long row = (long)blockIdx.x * 4 + wid; row < M; row += (long)gridDim.x * 4) {
-    const float mu = mean[row], rs = rstd[row];
-    const bf16_t* xr = x + row * D;
-    const bf16_t* dyr = dy + row * D;
-    float xh[NV][8], g[NV][8];
-    float s1 = 0.f, s2 = 0.f;
+  // two rows per iteration: both rows' loads are issued before either is reduced, so each wave
+  // keeps ~6 KB in flight instead of one row's dependent load -> reduce -> store chain
+  const long stride = (long)gridDim.x * 8;
+  for (long r0 = (long)blockIdx.x * 8 + wid; r0 < M; r0 += stride) {
+    const long rows[2] = {r0, r0 + 4};
+    float xv[2][NV][8], g[2][NV][8], rv[2][NV][8], mu[2], rs[2];
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c = (i * 64 + lane) * 8;
-      if (c < D) {
-        float xv[8];
-        unpack8(ld16(xr + c), xv);
-        unpack8(ld16(dyr + c), g[i]);
+    for (int u = 0; u < 2; ++u) {
+      const long row = rows[u] < M ? rows[u] : rows[0];
+      mu[u] = mean[row];
+      rs[u] = rstd[row];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          xh[i][j] = (xv[j] - mu) * rs;
-          const float gw = g[i][j] * wf[i][j];
-          s1 += gw;
-          s2 += gw * xh[i][j];
-          gacc[i][j] += g[i][j] * xh[i][j];
-          bacc[i][j] += g[i][j];
+      for (int i = 0; i < NV; ++i) {
+        const int c = (i * 64 + lane) * 8;
+        if (c < D) {
+          unpack8(ld16(x + row * D + c), xv[u][i]);
+          unpack8(ld16(dy + row * D + c), g[u][i]);
+          if (dres) unpack8(ld16(dres + row * D + c), rv[u][i]);
         }
       }
     }
-    s1 = wave_sum(s1) / D;
-    s2 = wave_sum(s2) / D;
-    bf16_t* dxr = dx + row * D;
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c = (i * 64 + lane) * 8;
-      if (c < D) {
-        float o[8], r[8];
+    for (int u = 0; u < 2; ++u) {
+      if (rows[u] >= M) break;
+      const long row = rows[u];
+      float xh[NV][8];
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = rs * (g[i][j] * wf[i][j] - s1 - xh[i][j] * s2);
-        if (dres) {  // fused residual-branch gradient: dx = LN'(dy) + dres
-          unpack8(ld16(dres + row * D + c), r);
+      for (int i = 0; i < NV; ++i) {
+        const int c = (i * 64 + lane) * 8;
+        if (c < D) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += r[j];
+          for (int j = 0; j < 8; ++j) {
+            xh[i][j] = (xv[u][i][j] - mu[u]) * rs[u];
+            const float gw = g[u][i][j] * wf[i][j];
+            s1 += gw;
+            s2 += gw * xh[i][j];
+            gacc[i][j] += g[u][i][j] * xh[i][j];
+            bacc[i][j] += g[u][i][j];
+          }
         }
-        st16(dxr + c, pack8(o));
+      }
+      s1 = wave_sum(s1) / D;
+      s2 = wave_sum(s2) / D;
+      bf16_t* dxr = dx + row * D;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c = (i * 64 + lane) * 8;
+        if (c < D) {
+          float o[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = rs[u] * (g[u][i][j] * wf[i][j] - s1 - xh[i][j] * s2);
+          if (dres) {  // fused residual-branch gradient: dx = LN'(dy) + dres
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] += rv[u][i][j];
+          }
+          st16(dxr + c, pack8(o));
+        }
       }
     }
   }
@@ -169,7 +187,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
 
 namespace mg {
 
-int ln_bwd_grid(int M) { return M / 4 < 2048 ? (M + 3) / 4 : 2048; }  // 8 waves/CU in flight
+int ln_bwd_grid(int M) { return M / 8 < 1024 ? (M + 7) / 8 : 1024; }  // 2 rows per wave-iteration
 
 #define MG_LN_DISPATCH(KERNEL, ...)                                                   \
   do {                                                                                \

@@ -9,6 +9,14 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+@pytest.fixture(autouse=True, params=[0, 1], ids=["bwd256", "bwd128"])
+def bwd_variant(request):
+    """Run every test under both backward kernels (256-key and 128-key workgroups)."""
+    ext().attention_set_bwd_variant(request.param)
+    yield request.param
+    ext().attention_set_bwd_variant(0)
+
+
 def _split(qkv, B, T, H):
     D = qkv.shape[-1] // 3
     q, k, v = qkv.float().view(B, T, 3 * D).split(D, dim=2)
@@ -125,3 +133,20 @@ def test_attention_dropout_exact(T):
     g = qkv_r.grad
     scale = g.abs().max().item()
     torch.testing.assert_close(dqkv.float(), g, atol=3e-2 * max(1.0, scale / 4), rtol=5e-2)
+
+
+def test_attention_dropout_keep_rate():
+    """The forward's counter-hash dropout keeps ~(1 - thr/256) of the causal entries, uniformly."""
+    C = ext()
+    B, T, H, hd, p = 2, 512, 4, 64, 0.1
+    qkv = torch.randn(B * T, 3 * H * hd, device=DEV).to(torch.bfloat16)
+    _, _, mask = C.attention_fwd(qkv, B, T, H, p, 5)
+    keep = _dense_keep(mask, B, T, H)
+    causal = torch.ones(T, T, dtype=torch.bool, device=DEV).tril()
+    rate = keep[..., causal].mean().item()
+    assert abs(rate - (1 - round(p * 256) / 256)) < 0.005
+    # no structure across heads / rows: per-head rates agree
+    per_head = keep[..., causal].mean(-1).flatten()
+    assert (per_head - rate).abs().max().item() < 0.01
+    _, _, mask2 = C.attention_fwd(qkv, B, T, H, p, 6)
+    assert (keep != _dense_keep(mask2, B, T, H))[..., causal].float().mean().item() > 0.1  # seed matters
