@@ -197,6 +197,19 @@ at::Tensor gelu_bwd(const at::Tensor& dy, const at::Tensor& pre) {
   return dx;
 }
 
+// dst[C, ldd] = src[R, C]^T with columns R..ldd-1 zero (ldd = 0 -> R)
+at::Tensor transpose(const at::Tensor& src, int64_t ldd) {
+  CHECK_BF16(src); CHECK_CONTIG(src);
+  TORCH_CHECK(src.dim() == 2, "transpose: 2-D input");
+  const int64_t R = src.size(0), C = src.size(1);
+  if (ldd <= 0) ldd = R;
+  TORCH_CHECK(ldd >= R, "transpose: ldd < rows");
+  DevGuard g(src.device());
+  auto dst = at::empty({C, ldd}, src.options());
+  mg::transpose(bp(src), bp(dst), (int)R, (int)C, (int)ldd, cur_stream());
+  return dst;
+}
+
 // residual-stream dropout backward: the mask is keyed on (row, column) of the [.., N] tensor
 at::Tensor dropout_bwd(const at::Tensor& dy, double p, int64_t seed) {
   CHECK_BF16(dy); CHECK_CONTIG(dy);
@@ -362,6 +375,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_dropout_residual", &bias_dropout_residual);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("dropout_bwd", &dropout_bwd);
+  m.def("transpose", &transpose);
   m.def("attention_set_bwd_variant", &mg::attention_set_bwd_variant);
   m.def("bias_grad", &bias_grad);
   m.def("dropout_bias_grad", &dropout_bias_grad);

@@ -46,6 +46,7 @@ void bias_dropout_residual(const bf16_t* x, const bf16_t* b, const bf16_t* r, bf
                            int N, float p, uint64_t seed, hipStream_t stream);
 void gelu_bwd(const bf16_t* dy, const bf16_t* pre, bf16_t* dx, long n, hipStream_t stream);
 void dropout_bwd(const bf16_t* dy, bf16_t* dx, long M, int N, float p, uint64_t seed, hipStream_t stream);
+void transpose(const bf16_t* src, bf16_t* dst, int R, int C, int ldd, hipStream_t stream);
 void bias_grad(const bf16_t* dy, float* db, long M, int N, hipStream_t stream);
 void dropout_bias_grad(const bf16_t* dy, bf16_t* dx, float* db, long M, int N, float p, uint64_t seed,
                        hipStream_t stream);

@@ -149,6 +149,61 @@ __global__ __launch_bounds__(256) void bias_grad_kernel(const bf16_t* __restrict
   }
 }
 
+// dst[c][r] = src[r][c] for a [R, C] bf16 matrix; dst rows have ldd >= R elements, the columns
+// R..ldd-1 are zero-filled (padded-K operands).  128x128 tiles, 256 threads: thread (rb, cb) loads
+// the 8x8 block at rows 8rb.., cols 8cb.. with 16-byte loads (16 threads = 256 contiguous bytes of a
+// row), transposes it in registers (one v_perm_b32 per output dword), and swaps blocks through
+// LDS (16-byte units, XOR-swizzled) so the stores are 16 threads x 16 B of one output row.
+__global__ __launch_bounds__(256) void transpose_kernel(const bf16_t* __restrict__ src,
+                                                        bf16_t* __restrict__ dst, int R, int C,
+                                                        int ldd) {
+  __shared__ uint4 t[16 * 8 * 16];  // [cb][k][rb ^ cb]
+  const int r0 = blockIdx.y * 128, c0 = blockIdx.x * 128;
+  {
+    const int rb = threadIdx.x >> 4, cb = threadIdx.x & 15;
+    uint32_t w[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = r0 + 8 * rb + i, c = c0 + 8 * cb;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (r < R) {
+        if (c + 8 <= C) {
+          v = ld16(src + (long)r * C + c);
+        } else if (c < C) {
+          alignas(16) bf16_t e[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+          for (int q = 0; q < 8 && c + q < C; ++q) e[q] = src[(long)r * C + c + q];
+          v = *reinterpret_cast<const uint4*>(e);
+        }
+      }
+      w[i][0] = v.x; w[i][1] = v.y; w[i][2] = v.z; w[i][3] = v.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // output row k of the block = input column k
+      uint32_t o[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+        o[d] = __builtin_amdgcn_perm(w[2 * d + 1][k >> 1], w[2 * d][k >> 1], (k & 1) ? 0x07060302u : 0x05040100u);
+      t[(cb * 8 + k) * 16 + (rb ^ cb)] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  }
+  __syncthreads();
+  const int cb = threadIdx.x >> 4, rb = threadIdx.x & 15;
+  const int r = r0 + 8 * rb;
+  if (r >= ldd) return;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = c0 + 8 * cb + k;
+    if (c >= C) break;
+    const uint4 v = t[(cb * 8 + k) * 16 + (rb ^ cb)];
+    if (r + 8 <= ldd) {
+      st16(dst + (long)c * ldd + r, v);
+    } else {
+      const bf16_t* e = reinterpret_cast<const bf16_t*>(&v);
+      for (int q = 0; r + q < ldd; ++q) dst[(long)c * ldd + r + q] = e[q];
+    }
+  }
+}
+
 int grid_for(long n8) { return (int)std::min<long>(kGrid, (n8 + 255) / 256); }
 
 }  // namespace
@@ -188,6 +243,10 @@ void dropout_bias_grad(const bf16_t* dy, bf16_t* dx, float* db, long M, int N, f
   const uint32_t thr = dropout_threshold8(p);
   dropout_bias_grad_kernel<<<dim3(cx, ry), 256, 0, stream>>>(dy, dx, db, (int)M, N, seed, thr,
                                                              dropout_scale8(thr));
+}
+
+void transpose(const bf16_t* src, bf16_t* dst, int R, int C, int ldd, hipStream_t stream) {
+  transpose_kernel<<<dim3(cdiv(C, 128), cdiv(ldd, 128)), 256, 0, stream>>>(src, dst, R, C, ldd);
 }
 
 void bias_grad(const bf16_t* dy, float* db, long M, int N, hipStream_t stream) {

@@ -80,7 +80,7 @@ struct GemmArgs {
 };
 
 static unsigned long long* g_dbg = nullptr;  // MG_GEMM_STAMPS builds: stamp buffer
-static int g_variant = 0;  // 0 auto, 1 force T128, 2 force T256, 3 force T2x1, 4 force PP, 5 force W4
+static int g_variant = 0;  // 0 auto, 1 force T128, 2 force T256, 3 force T2x1, 4 force PP, 5 force W4, 6 force W4 BN=192
 
 MG_DEVICE int swz_mn(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 
@@ -271,8 +271,10 @@ MG_DEVICE void epilogue(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int 
         }
         if constexpr (EPI == 3) {
           if (args.thr) {  // one Philox call per 64-column block of this lane's row (common.h rowdrop)
-            if ((j & 3) == 0) rnd = rowdrop_call(args.seed, m, n, args.N);
-            rowdrop4(v, word_of(rnd, j & 3), args.thr, args.scale);
+            // (wave tiles 64 / 128 wide start on a 64-column block; the 96-wide W4 tile may not)
+            const int w16 = (n >> 4) & 3;
+            if (CF::WTN % 64 == 0 ? (j & 3) == 0 : (j == 0 || w16 == 0)) rnd = rowdrop_call(args.seed, m, n, args.N);
+            rowdrop4(v, word_of(rnd, CF::WTN % 64 == 0 ? (j & 3) : w16), args.thr, args.scale);
           }
           v[0] += bf2f(side[j].x & 0xffffu); v[1] += bf2f(side[j].x >> 16);
           v[2] += bf2f(side[j].y & 0xffffu); v[3] += bf2f(side[j].y >> 16);
@@ -661,15 +663,23 @@ MG_DEVICE void mfma_acc(f32x4& acc, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b) : "memory");
 }
 
-namespace w4k {
-constexpr int STAGE = 65536;          // one K-tile: A 32 KiB + B 32 KiB (T256 images)
-constexpr int SINK = 2 * STAGE;       // DMA past the last K-tile lands here (never read)
-constexpr int SMEM = 2 * STAGE + 32768;
-}  // namespace w4k
+// BN = 256 (128x128 wave tiles) or 192 (128x96: 2 rounds instead of 1.5 for N = 768 on 256 CUs;
+// k-contiguous B only -- the m/n-contiguous half-images are 128 columns wide)
+template <int BN>
+struct W4 {
+  static constexpr int FN = BN / 32;                  // 16-col fragments per wave (2 x 2 waves)
+  static constexpr int STAGE = 32768 + BN * 128;      // one K-tile: A 32 KiB + B BN x 128 B
+  static constexpr int SINK = 2 * STAGE;              // DMA past the last K-tile lands here
+  static constexpr int SMEM = 2 * STAGE + 32768;
+  static constexpr int NR = 8 + FN;                   // fragment reads / DMA pieces per phase
+};
 
-template <bool AK, bool BKC, int EPI, bool OUTF32>
+template <int BN, bool AK, bool BKC, int EPI, bool OUTF32>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
-  using CF = Cfg<256, 256, 2, 2>;
+  static_assert(BN == 256 || BKC, "W4 with BN != 256 needs a k-contiguous B operand");
+  using CF = Cfg<256, BN, 2, 2>;
+  using WK = W4<BN>;
+  constexpr int FN = WK::FN, NR = WK::NR, NQ = 8 * FN;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -685,49 +695,49 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
   const int first_m = (wg / group) * GROUP_M;
   const int gm = min(args.tiles_m - first_m, GROUP_M);
   const int m0 = (first_m + (wg % group) % gm) * 256;
-  const int n0 = ((wg % group) / gm) * 256;
+  const int n0 = ((wg % group) / gm) * BN;
 
-  f32x4 acc[8][8];
+  f32x4 acc[8][FN];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int kbeg = split * args.kchunk;
   const int nk = (min(args.K, kbeg + args.kchunk) - kbeg + BK - 1) / BK;
   Stager<AK, 256, 4> sta;
-  Stager<BKC, 256, 4> stb;
+  Stager<BKC, BN, 4> stb;
   sta.init(args.A, args.a_bytes, args.lda, m0, args.a_ext, kbeg, args.ka, kbeg + args.kchunk, wid, lane);
   stb.init(args.B, args.b_bytes, args.ldb, n0, args.b_ext, kbeg, args.kb, kbeg + args.kchunk, wid, lane);
   sta.stage(smem, 0);
   stb.stage(smem + CF::A_BYTES, 0);
   if (nk > 1) {
-    sta.stage(smem + w4k::STAGE, 1);
-    stb.stage(smem + w4k::STAGE + CF::A_BYTES, 1);
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    sta.stage(smem + WK::STAGE, 1);
+    stb.stage(smem + WK::STAGE + CF::A_BYTES, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NR) : "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
-  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+  bf16x8 fa0[8], fb0[FN], fa1[8], fb1[FN];
 #pragma unroll
   for (int i = 0; i < 8; ++i) fa0[i] = frag<AK>(smem, wm * 8 + i, 0, lane);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) fb0[j] = frag<BKC>(smem + CF::A_BYTES, wn * 8 + j, 0, lane);
+  for (int j = 0; j < FN; ++j) fb0[j] = frag<BKC>(smem + CF::A_BYTES, wn * FN + j, 0, lane);
 
   for (int kt = 0; kt < nk; ++kt) {
-    const char* sa = smem + (kt & 1) * w4k::STAGE;
+    const char* sa = smem + (kt & 1) * WK::STAGE;
     // phase A: k32 step 0 of tile kt; step-1 fragments read between the MFMAs (one per 2)
 #pragma unroll
-    for (int q = 0; q < 64; ++q) {
-      const int i = q >> 3, j = q & 7;
+    for (int q = 0; q < NQ; ++q) {
+      const int i = q / FN, j = q % FN;
       mfma_acc(acc[i][j], fb0[j], fa0[i]);
-      if ((q & 1) == 0 && q < 32) {
-        const int r = q >> 1;  // 0..15: A fragments then B fragments
+      if ((q & 1) == 0 && q < 2 * NR) {
+        const int r = q >> 1;  // A fragments then B fragments
         if (r < 8) fa1[r] = frag<AK>(sa, wm * 8 + r, 1, lane);
-        else fb1[r - 8] = frag<BKC>(sa + CF::A_BYTES, wn * 8 + r - 8, 1, lane);
+        else fb1[r - 8] = frag<BKC>(sa + CF::A_BYTES, wn * FN + r - 8, 1, lane);
       }
     }
     // tile kt+1 landed (this wave's DMA), every wave done reading buffer kt & 1
@@ -738,22 +748,23 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
     // step-0 fragments of tile kt+1 between the MFMAs
     const int t2 = kt + 2;
     const int tt = t2 < nk ? t2 : 0;
-    char* dst = t2 < nk ? smem + (kt & 1) * w4k::STAGE : smem + w4k::SINK;
+    char* dst = t2 < nk ? smem + (kt & 1) * WK::STAGE : smem + WK::SINK;
     const __amdgpu_buffer_rsrc_t ra = sta.rsrc(tt), rb = stb.rsrc(tt);
-    const char* sn = smem + ((kt + 1) & 1) * w4k::STAGE;
+    const char* sn = smem + ((kt + 1) & 1) * WK::STAGE;
+    constexpr int QR = NQ - 2 * NR;  // fragment reads in the odd slots of the last 2*NR MFMAs
 #pragma unroll
-    for (int q = 0; q < 64; ++q) {
-      const int i = q >> 3, j = q & 7;
+    for (int q = 0; q < NQ; ++q) {
+      const int i = q / FN, j = q % FN;
       mfma_acc(acc[i][j], fb1[j], fa1[i]);
-      if (q < 32 && (q & 1) == 0) {
-        const int r = q >> 1;  // 16 DMA pieces: 8 of A, 8 of B
+      if (q < 2 * NR && (q & 1) == 0) {
+        const int r = q >> 1;  // DMA pieces: 8 of A, FN of B
         if (r < 8) sta.piece(dst, ra, tt, r);
         else stb.piece(t2 < nk ? dst + CF::A_BYTES : dst, rb, tt, r - 8);
       }
-      if (q >= 32 && (q & 1) == 0) {
-        const int r = (q - 32) >> 1;  // 16 fragment reads of tile kt+1 step 0
+      if (q >= QR && ((q - QR) & 1) == 1) {
+        const int r = (q - QR) >> 1;  // fragment reads of tile kt+1 step 0
         if (r < 8) fa0[r] = frag<AK>(sn, wm * 8 + r, 0, lane);
-        else fb0[r - 8] = frag<BKC>(sn + CF::A_BYTES, wn * 8 + r - 8, 0, lane);
+        else fb0[r - 8] = frag<BKC>(sn + CF::A_BYTES, wn * FN + r - 8, 0, lane);
       }
     }
   }
@@ -762,21 +773,25 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
   epilogue<CF, EPI, OUTF32>(args, acc, m0, n0, wm, wn, wid, lane, smem);
 }
 
-template <bool AK, bool BKC, int EPI, bool OUTF32>
+template <int BN, bool AK, bool BKC, int EPI, bool OUTF32>
 void launch_w4(GemmArgs a, hipStream_t stream) {
-  a.tiles_m = cdiv(a.M, 256);
-  a.tiles_n = cdiv(a.N, 256);
-  a.splits = 1;
-  a.kchunk = cdiv(a.K, BK) * BK;
-  if (OUTF32) set_split(a, 256, 6);
-  const int grid = a.tiles_m * a.tiles_n * a.splits;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)gemm_w4_kernel<AK, BKC, EPI, OUTF32>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, w4k::SMEM);
-    attr_set = true;
+  if constexpr (BN != 256 && !BKC) {
+    launch_w4<256, AK, BKC, EPI, OUTF32>(a, stream);
+  } else {
+    a.tiles_m = cdiv(a.M, 256);
+    a.tiles_n = cdiv(a.N, BN);
+    a.splits = 1;
+    a.kchunk = cdiv(a.K, BK) * BK;
+    if (OUTF32) set_split(a, 256, 6);
+    const int grid = a.tiles_m * a.tiles_n * a.splits;
+    static bool attr_set = false;
+    if (!attr_set) {
+      hipFuncSetAttribute((const void*)gemm_w4_kernel<BN, AK, BKC, EPI, OUTF32>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, W4<BN>::SMEM);
+      attr_set = true;
+    }
+    gemm_w4_kernel<BN, AK, BKC, EPI, OUTF32><<<grid, 256, W4<BN>::SMEM, stream>>>(a);
   }
-  gemm_w4_kernel<AK, BKC, EPI, OUTF32><<<grid, 256, w4k::SMEM, stream>>>(a);
 }
 
 template <class CF, bool AK, bool BKC, int EPI, bool OUTF32>
@@ -806,8 +821,14 @@ void launch(GemmArgs a, hipStream_t stream) {
 // count quantises badly onto the 256 CUs.
 int pick_config(int M, int N, int K, int layout) {
   if (g_variant) return g_variant;
-  const long t256 = (long)cdiv(M, 256) * cdiv(N, 256);
-  if (layout == 0) return (t256 >= 768 || (t256 >= 384 && K >= 2048)) ? 5 : 1;
+  const long tm = cdiv(M, 256);
+  const long t256 = tm * cdiv(N, 256);
+  if (layout == 0) {
+    if (!(t256 >= 768 || (t256 >= 384 && K >= 2048))) return 1;
+    // W4 width: fewer (rounds x tile width) on the 256 CUs wins; ties go to the wider tile
+    const long r256 = (t256 + 255) / 256 * 256, r192 = (tm * cdiv(N, 192) + 255) / 256 * 192;
+    return r192 < r256 ? 6 : 5;
+  }
   if (layout == 1) return (K >= 1536 || t256 >= 1024) ? 4 : 1;
   return (long)M * N >= (1L << 20) ? 4 : 1;
 }
@@ -819,7 +840,8 @@ void dispatch(const GemmArgs& a, hipStream_t stream) {
     case 2: launch<T256, AK, BKC, EPI, OUTF32>(a, stream); break;
     case 3: launch<T2x1, AK, BKC, EPI, OUTF32>(a, stream); break;
     case 4: launch_pp<AK, BKC, EPI, OUTF32>(a, stream); break;
-    case 5: launch_w4<AK, BKC, EPI, OUTF32>(a, stream); break;
+    case 5: launch_w4<256, AK, BKC, EPI, OUTF32>(a, stream); break;
+    case 6: launch_w4<192, AK, BKC, EPI, OUTF32>(a, stream); break;
     default: launch<T128, AK, BKC, EPI, OUTF32>(a, stream); break;
   }
 }
@@ -852,7 +874,8 @@ void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long l
     if (epi == 0) dispatch<true, true, 0, false>(a, stream);
     else if (epi == 1) dispatch<true, true, 1, false>(a, stream);
     else if (epi == 2) dispatch<true, true, 2, false>(a, stream);
-    else dispatch<true, true, 3, false>(a, stream);
+    else if (epi == 3) dispatch<true, true, 3, false>(a, stream);
+    else dispatch<true, true, 4, false>(a, stream);  // dgrad as NT against a transposed weight
   } else if (layout == 1) {
     if (epi == 4) dispatch<true, false, 4, false>(a, stream);
     else dispatch<true, false, 0, false>(a, stream);

@@ -94,10 +94,10 @@ class TransformerBlockFn(torch.autograd.Function):
             dz = dx2
             C.bias_grad(dz, g[id(bp)][0])
         G.gemm_tn_acc(dz, u, g[id(wp)][0])
-        dpre = G.gemm_nn(dz, wp, epi="gelu_bwd", aux=pre)
+        dpre = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=pre)
         G.gemm_tn_acc(dpre, h2, g[id(wfc)][0])
         C.bias_grad(dpre, g[id(bfc)][0])
-        dh2 = G.gemm_nn(dpre, wfc)
+        dh2 = G.gemm_dgrad(dpre, wfc)
         dx1 = C.layernorm_bwd(dh2, x1, ln2w, mean2, rstd2, g[id(ln2w)][0], g[id(ln2b)][0], dx2)
         # ---- attention: x1 = x + drop(attn(h Wqkv^T + bqkv) Wo^T + bo)
         if p_resid > 0:
@@ -106,11 +106,11 @@ class TransformerBlockFn(torch.autograd.Function):
             dz = dx1
             C.bias_grad(dz, g[id(bo)][0])
         G.gemm_tn_acc(dz, y, g[id(wo)][0])
-        dy = G.gemm_nn(dz, wo)
+        dy = G.gemm_dgrad(dz, wo)
         dqkv = C.attention_bwd(qkv, y, dy, lse, amask, B, T, H, float(p_attn), ctx.seeds[0])
         G.gemm_tn_acc(dqkv, h, g[id(wqkv)][0])
         C.bias_grad(dqkv, g[id(bqkv)][0])
-        dh = G.gemm_nn(dqkv, wqkv)
+        dh = G.gemm_dgrad(dqkv, wqkv)
         dx = C.layernorm_bwd(dh, x, ln1w, mean1, rstd1, g[id(ln1w)][0], g[id(ln1b)][0], dx1)
         outs = [finish(prm, *g[id(prm)]) for prm in ctx.params]
         return (dx, *outs, None)
@@ -148,7 +148,7 @@ class HeadLossFn(torch.autograd.Function):
         del logits
         bw, mw = grad_target(w)
         G.gemm_tn_acc(dlogits, h, bw, n_valid=V)
-        dh = G.gemm_nn(dlogits, w)
+        dh = G.gemm_dgrad(dlogits, w)  # W^T padded to the logits' row stride (zero columns)
         blw, mlw = grad_target(lnw)
         blb, mlb = grad_target(lnb)
         dx = C.layernorm_bwd(dh, x, lnw, mean, rstd, blw, blb, None)

@@ -28,19 +28,37 @@ def _check2d(t, name):
 
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: Optional[torch.Tensor] = None,
             epi: str = "none", resid: Optional[torch.Tensor] = None, p: float = 0.0, seed: int = 0,
-            pre_out: Optional[torch.Tensor] = None, ld: Optional[int] = None) -> torch.Tensor:
-    """C = A @ B^T with a fused epilogue. ``ld`` pads the output row stride (logits)."""
+            pre_out: Optional[torch.Tensor] = None, ld: Optional[int] = None,
+            aux: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """C = A @ B^T with a fused epilogue. ``ld`` pads the output row stride (logits).
+    ``gelu_bwd`` (data gradient against a transposed weight) multiplies by GELU'(aux)."""
     _check2d(a, "A")
     _check2d(b, "B")
     M, K = a.shape
     N = b.shape[0]
     ld = ld or N
     c = torch.empty((M, ld), dtype=torch.bfloat16, device=a.device)
-    code = {"none": EPI_NONE, "bias": EPI_BIAS, "gelu": EPI_GELU, "resid": EPI_RESID}[epi]
+    code = {"none": EPI_NONE, "bias": EPI_BIAS, "gelu": EPI_GELU, "resid": EPI_RESID,
+            "gelu_bwd": EPI_GELU_BWD}[epi]
     if code == EPI_BIAS and bias is None:
         code = EPI_NONE
-    ext().gemm(a, b, c, 0, code, bias, pre_out, resid, float(p), int(seed), M, N)
+    ext().gemm(a, b, c, 0, code, bias, aux if code == EPI_GELU_BWD else pre_out, resid, float(p),
+               int(seed), M, N)
     return c
+
+
+def transpose(w: torch.Tensor, ld: Optional[int] = None) -> torch.Tensor:
+    """W^T as a contiguous [cols, ld] bf16 tensor (columns >= rows zero): the B operand that turns a
+    data gradient dX = dY @ W into the NT layout (both operands k-contiguous, the fast GEMM path)."""
+    return ext().transpose(w, int(ld or 0))
+
+
+def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, *, epi: str = "none",
+               aux: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dX = dY @ W (W [N_out, N_in] as stored by nn.Linear), as NT against W^T."""
+    if wt is None:
+        wt = transpose(w, dy.shape[1])
+    return gemm_nt(dy, wt, epi=epi, aux=aux)
 
 
 def gemm_nn(a: torch.Tensor, b: torch.Tensor, *, epi: str = "none",

@@ -9,7 +9,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.fixture(autouse=True, params=[0, 1, 2, 3, 4, 5], ids=["auto", "t128", "t256", "t256x128", "pp256", "w4"])
+@pytest.fixture(autouse=True, params=[0, 1, 2, 3, 4, 5, 6], ids=["auto", "t128", "t256", "t256x128", "pp256", "w4", "w4n192"])
 def tile_config(request):
     """Run every GEMM test under each tile configuration of gemm.hip (0 = per-shape choice)."""
     from mingpt_distributed_amd.ops._ext import ext
@@ -98,3 +98,26 @@ def test_tn_acc_nvalid():
     c = torch.zeros(V, K, device=DEV)
     G.gemm_tn_acc(a, b, c, n_valid=V)
     _check(c, a.float()[:, :V].t() @ b.float(), Mr)
+
+
+@pytest.mark.parametrize("R,C,ld", [(768, 2304, 768), (130, 72, 136), (1001, 64, 1008)])
+def test_transpose_padded(R, C, ld):
+    w = _bf(R, C, seed=17)
+    t = G.transpose(w, ld)
+    assert t.shape == (C, ld)
+    torch.testing.assert_close(t[:, :R], w.t(), rtol=0, atol=0)
+    assert (t[:, R:] == 0).all()
+
+
+@pytest.mark.parametrize("M,Nout,Nin", [(1000, 2304, 768), (256, 768, 3072), (130, 1001, 64)])
+def test_dgrad_nt(M, Nout, Nin):
+    """dX = dY @ W through the NT path against W^T (padded reduction for the vocab case)."""
+    ld = (Nout + 7) // 8 * 8
+    dy = _bf(M, ld, seed=18)
+    dy[:, Nout:] = 0
+    w = _bf(Nout, Nin, seed=19)
+    ref = dy.float()[:, :Nout] @ w.float()
+    _check(G.gemm_dgrad(dy, w), ref, Nout)
+    pre = _bf(M, Nin, seed=20)
+    _check(G.gemm_dgrad(dy, w, epi="gelu_bwd", aux=pre),
+           ref * torch.func.grad(lambda x: R.gelu_tanh(x).sum())(pre.float()), Nout)
