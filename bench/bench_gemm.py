@@ -14,7 +14,7 @@ import torch
 from mingpt_distributed_amd.ops import gemm as G
 
 
-VARIANTS = ("auto", "t128", "t256", "t256x128", "pp256", "w4")
+VARIANTS = ("auto", "t128", "t256", "t256x128", "pp256", "w4", "w4n192")
 
 
 def timeit(fn, iters=20, warm=3):
@@ -83,6 +83,18 @@ def main():
               flush=True)
     print(json.dumps({"total_mine_ms": round(tot_m, 3), "total_hipblaslt_ms": round(tot_b, 3)}))
     print(json.dumps({"variant_ms(" + ",".join(VARIANTS) + ")": {f"{k[0]}:{k[1]}": [round(t, 4) for t in v] for k, v in variants.items()}}))
+    # fused-epilogue shapes of the step (forward and NT data-gradient forms), all tile configs
+    epi = {}
+    bias3, bias4 = r(3 * D), r(4 * D)
+    x, wq, wfc, wp = r(M, D), r(3 * D, D), r(4 * D, D), r(D, 4 * D)
+    u, pre = r(M, 4 * D), torch.empty(M, 4 * D, device="cuda", dtype=torch.bfloat16)
+    dz, wpt = r(M, D), G.transpose(wp, D)
+    _, epi["qkv_bias"] = both(lambda: G.gemm_nt(x, wq, bias=bias3, epi="bias"))
+    _, epi["fc_gelu"] = both(lambda: G.gemm_nt(x, wfc, bias=bias4, epi="gelu", pre_out=pre))
+    _, epi["proj_resid_drop"] = both(lambda: G.gemm_nt(u, wp, bias=r(D), epi="resid", resid=x, p=0.1, seed=3))
+    _, epi["dgrad_gelu_bwd_nt"] = both(lambda: G.gemm_nt(dz, wpt, epi="gelu_bwd", aux=pre))
+    _, epi["dgrad_fc_nt"] = both(lambda: G.gemm_dgrad(u, wfc, wt=G.transpose(wfc, 4 * D)))
+    print(json.dumps({"epilogue_ms(" + ",".join(VARIANTS) + ")": {k: [round(t, 4) for t in v] for k, v in epi.items()}}))
     for n in (4096, 8192):
         a4, b4 = r(n, n), r(n, n)
         t4, v4 = both(lambda: G.gemm_nt(a4, b4))

@@ -181,11 +181,10 @@ MG_DEVICE float gelu_sigmoid(float x) {  // sigmoid(2u)
 MG_DEVICE float gelu_f(float x) { return x * gelu_sigmoid(x); }
 
 // d/dx [x s(x)], s = sigmoid(2u): s + 2 x s (1 - s) K0 (1 + 3 K1 x^2)
-MG_DEVICE float gelu_grad(float x) {
-  const float x2 = x * x;
-  const float sg = gelu_sigmoid(x);
-  return sg + 2.f * x * sg * (1.f - sg) * kGeluK0 * __builtin_fmaf(3.f * kGeluK1, x2, 1.f);
+MG_DEVICE float gelu_grad_from(float x, float sg) {
+  return __builtin_fmaf(2.f * kGeluK0 * x * sg * (1.f - sg), __builtin_fmaf(3.f * kGeluK1, x * x, 1.f), sg);
 }
+MG_DEVICE float gelu_grad(float x) { return gelu_grad_from(x, gelu_sigmoid(x)); }
 
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 

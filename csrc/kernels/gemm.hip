@@ -26,7 +26,8 @@
 //  * XCD-aware bijective block remap + GROUP_M ordering (blocks sharing A rows share an XCD's L2).
 //  * epilogues: none | +bias | +bias,GELU (pre-activation also stored) |
 //    resid + dropout(acc + bias) (Philox mask, same element mapping as elementwise.hip) |
-//    acc * GELU'(pre) | fp32 accumulate (the main-grad buffer), split-K via LDS-staged atomics.
+//    acc * aux (GELU' from the forward) | fp32 accumulate (the main-grad buffer), split-K via
+//    LDS-staged atomics.
 #include "common.h"
 #include "kernels.h"
 
@@ -264,10 +265,15 @@ MG_DEVICE void epilogue(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int 
           v[0] += bf2f(bs[j].x & 0xffffu); v[1] += bf2f(bs[j].x >> 16);
           v[2] += bf2f(bs[j].y & 0xffffu); v[3] += bf2f(bs[j].y >> 16);
         }
-        if constexpr (EPI == 2) {
-          *reinterpret_cast<uint2*>(args.aux + off) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        if constexpr (EPI == 2) {  // y = GELU(z); aux <- GELU'(z) for the backward (one multiply there)
+          float gd[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = gelu_f(v[r]);
+          for (int r = 0; r < 4; ++r) {
+            const float sg = gelu_sigmoid(v[r]);
+            gd[r] = gelu_grad_from(v[r], sg);
+            v[r] *= sg;
+          }
+          *reinterpret_cast<uint2*>(args.aux + off) = make_uint2(pack2(gd[0], gd[1]), pack2(gd[2], gd[3]));
         }
         if constexpr (EPI == 3) {
           if (args.thr) {  // one Philox call per 64-column block of this lane's row (common.h rowdrop)
@@ -279,9 +285,9 @@ MG_DEVICE void epilogue(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int 
           v[0] += bf2f(side[j].x & 0xffffu); v[1] += bf2f(side[j].x >> 16);
           v[2] += bf2f(side[j].y & 0xffffu); v[3] += bf2f(side[j].y >> 16);
         }
-        if constexpr (EPI == 4) {
-          v[0] *= gelu_grad(bf2f(side[j].x & 0xffffu)); v[1] *= gelu_grad(bf2f(side[j].x >> 16));
-          v[2] *= gelu_grad(bf2f(side[j].y & 0xffffu)); v[3] *= gelu_grad(bf2f(side[j].y >> 16));
+        if constexpr (EPI == 4) {  // aux = GELU'(z) stored by the forward's EPI 2
+          v[0] *= bf2f(side[j].x & 0xffffu); v[1] *= bf2f(side[j].x >> 16);
+          v[2] *= bf2f(side[j].y & 0xffffu); v[3] *= bf2f(side[j].y >> 16);
         }
         *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(args.C) + off) =
             make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
@@ -824,10 +830,11 @@ int pick_config(int M, int N, int K, int layout) {
   const long tm = cdiv(M, 256);
   const long t256 = tm * cdiv(N, 256);
   if (layout == 0) {
-    if (!(t256 >= 768 || (t256 >= 384 && K >= 2048))) return 1;
-    // W4 width: fewer (rounds x tile width) on the 256 CUs wins; ties go to the wider tile
+    if (t256 < 256) return 1;
+    // W4 width: fewer (rounds x tile width) on the 256 CUs wins; the 96-wide wave tile costs ~8 %
+    // more per FLOP (more LDS reads per MFMA), so it must save more than that
     const long r256 = (t256 + 255) / 256 * 256, r192 = (tm * cdiv(N, 192) + 255) / 256 * 192;
-    return r192 < r256 ? 6 : 5;
+    return r192 * 108 < r256 * 100 ? 6 : 5;
   }
   if (layout == 1) return (K >= 1536 || t256 >= 1024) ? 4 : 1;
   return (long)M * N >= (1L << 20) ? 4 : 1;

@@ -67,10 +67,10 @@ class TransformerBlockFn(torch.autograd.Function):
         y, lse, amask = C.attention_fwd(qkv, B, T, H, float(p_attn), seeds[0])
         x1 = G.gemm_nt(y, wo, bias=bo, epi="resid", resid=x, p=p_resid, seed=seeds[1])
         h2, mean2, rstd2 = C.layernorm_fwd(x1, ln2w, ln2b, eps)
-        pre = torch.empty((x.shape[0], wfc.shape[0]), dtype=torch.bfloat16, device=x.device)
-        u = G.gemm_nt(h2, wfc, bias=bfc, epi="gelu", pre_out=pre)
+        gd = torch.empty((x.shape[0], wfc.shape[0]), dtype=torch.bfloat16, device=x.device)  # GELU'(z)
+        u = G.gemm_nt(h2, wfc, bias=bfc, epi="gelu", pre_out=gd)
         x2 = G.gemm_nt(u, wp, bias=bp, epi="resid", resid=x1, p=p_resid, seed=seeds[2])
-        ctx.save_for_backward(x, h, mean1, rstd1, qkv, y, lse, amask, x1, h2, mean2, rstd2, pre, u)
+        ctx.save_for_backward(x, h, mean1, rstd1, qkv, y, lse, amask, x1, h2, mean2, rstd2, gd, u)
         ctx.params = (ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, wfc, bfc, wp, bp)
         ctx.cfg, ctx.seeds = cfg, seeds
         for prm in ctx.params:
@@ -81,7 +81,7 @@ class TransformerBlockFn(torch.autograd.Function):
     def backward(ctx, dx2):
         B, T, H, p_attn, p_resid, eps = ctx.cfg
         C = ext()
-        x, h, mean1, rstd1, qkv, y, lse, amask, x1, h2, mean2, rstd2, pre, u = ctx.saved_tensors
+        x, h, mean1, rstd1, qkv, y, lse, amask, x1, h2, mean2, rstd2, gd, u = ctx.saved_tensors
         ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, wfc, bfc, wp, bp = ctx.params
         dx2 = dx2.contiguous()
         g = {}
@@ -94,7 +94,7 @@ class TransformerBlockFn(torch.autograd.Function):
             dz = dx2
             C.bias_grad(dz, g[id(bp)][0])
         G.gemm_tn_acc(dz, u, g[id(wp)][0])
-        dpre = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=pre)
+        dpre = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=gd)
         G.gemm_tn_acc(dpre, h2, g[id(wfc)][0])
         C.bias_grad(dpre, g[id(bfc)][0])
         dh2 = G.gemm_dgrad(dpre, wfc)

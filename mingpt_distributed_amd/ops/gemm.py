@@ -2,10 +2,11 @@
 epilogue fused where the data is produced.
 
 * ``gemm_nt``      C[M,N] = A[M,K] @ B[N,K]^T   (forward; B is an nn.Linear weight [out, in])
-                   epilogues: ``none`` | ``bias`` | ``gelu`` (bias + tanh-GELU, also stores the
-                   pre-activation) | ``resid`` (R + dropout(acc + bias))
+                   epilogues: ``none`` | ``bias`` | ``gelu`` (bias + tanh-GELU, also stores
+                   GELU'(z) for the backward) | ``resid`` (R + dropout(acc + bias)) |
+                   ``gelu_bwd`` (acc * aux, aux = the stored GELU')
 * ``gemm_nn``      C[M,N] = A[M,K] @ B[K,N]     (data gradient dX = dY @ W)
-                   epilogue: ``none`` | ``gelu_bwd`` (multiply by GELU'(pre))
+                   epilogue: ``none`` | ``gelu_bwd`` (multiply by aux = GELU'(z) from the forward)
 * ``gemm_tn_acc``  C[N,K] += A[M,N]^T @ B[M,K] (weight gradient, fp32 accumulate into main_grad)
 
 All three run on the hand-written MFMA kernel in ``csrc/kernels/gemm.hip`` (``_C.gemm``).
@@ -31,7 +32,7 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: Optional[torch.Tensor] = 
             pre_out: Optional[torch.Tensor] = None, ld: Optional[int] = None,
             aux: Optional[torch.Tensor] = None) -> torch.Tensor:
     """C = A @ B^T with a fused epilogue. ``ld`` pads the output row stride (logits).
-    ``gelu_bwd`` (data gradient against a transposed weight) multiplies by GELU'(aux)."""
+    ``gelu`` writes GELU'(z) into ``pre_out``; ``gelu_bwd`` multiplies by ``aux`` (that GELU')."""
     _check2d(a, "A")
     _check2d(b, "B")
     M, K = a.shape
@@ -63,7 +64,7 @@ def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, *, epi: str = "none",
 
 def gemm_nn(a: torch.Tensor, b: torch.Tensor, *, epi: str = "none",
             aux: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """C = A @ B (B row-major [K, N]); ``gelu_bwd`` multiplies by GELU'(aux)."""
+    """C = A @ B (B row-major [K, N]); ``gelu_bwd`` multiplies by ``aux`` (a stored GELU')."""
     _check2d(a, "A")
     _check2d(b, "B")
     M, K = a.shape
