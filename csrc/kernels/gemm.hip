@@ -105,15 +105,22 @@ template <bool KC, int R, int NW>
 struct Stager {
   static constexpr int PER = R / 8 / NW;  // 1-KiB pieces per wave (R*128 B per tile)
   uint32_t voff[PER];
+  const char* ptr;  // operand base
   const char* base;
-  uint32_t bytes, step;
-  int klim, tail_t, swid;
+  uint32_t total, bytes, step;
+  long ld;
+  int kbeg, klim, tail_t, swid;
 
-  MG_DEVICE void init(const bf16_t* ptr, uint32_t total, long ld, int r0, int ext, int kbeg, int kvalid,
+  // k-contiguous operands: per-lane offsets are relative to the tile's first row (the row origin is
+  // in the descriptor base, see retarget), so they are the same for every tile; rows past the
+  // operand read as zero through the descriptor extent (the operand buffer ends at its last row).
+  // m/n-contiguous operands: absolute offsets with a per-lane column check.
+  MG_DEVICE void init(const bf16_t* p, uint32_t tot, long ld_, int r0, int ext, int kbeg_, int kvalid,
                       int kend, int wid, int lane) {
-    const uint32_t k0b = KC ? (uint32_t)kbeg * 2 : (uint32_t)((long)kbeg * ld * 2);
-    base = reinterpret_cast<const char*>(ptr) + k0b;
-    bytes = total > k0b ? total - k0b : 0u;
+    ptr = reinterpret_cast<const char*>(p);
+    total = tot;
+    ld = ld_;
+    kbeg = kbeg_;
     step = KC ? BK * 2 : (uint32_t)(BK * ld * 2);
     klim = min(kvalid, kend) - kbeg;
     tail_t = klim / BK;
@@ -123,8 +130,7 @@ struct Stager {
       const int j = wid * PER + i;
       if constexpr (KC) {  // [R rows][128 B]: block = 8 rows x 8 chunks
         const int row = 8 * j + (lane >> 3), ch = (lane & 7) ^ (row & 7);
-        const int gr = r0 + row;
-        voff[i] = gr < ext ? (uint32_t)(((long)gr * ld + ch * 8) * 2) : kOOB;
+        voff[i] = (uint32_t)(((long)row * ld + ch * 8) * 2);
       } else {  // R/128 half-images [64 k][256 B]: block = 4 k-rows x 16 chunks
         const int half = j >> 4, jj = j & 15;
         const int row = 4 * jj + (lane >> 4), ch = (lane & 15) ^ swz_mn(row);
@@ -132,6 +138,13 @@ struct Stager {
         voff[i] = gc < ext ? (uint32_t)(((long)row * ld + gc) * 2) : kOOB;
       }
     }
+    retarget(r0);
+  }
+  // new tile origin (k-contiguous operands: scalar work only)
+  MG_DEVICE void retarget(int r0) {
+    const uint64_t o = KC ? (uint64_t)((long)r0 * ld + kbeg) * 2 : (uint64_t)kbeg * ld * 2;
+    base = ptr + o;
+    bytes = total > o ? total - (uint32_t)o : 0u;
   }
   // piece-level form for hand-interleaved schedules: descriptor once per tile, then piece(i)
   MG_DEVICE __amdgpu_buffer_rsrc_t rsrc(int t) const { return tile_rsrc(base, bytes, step, t); }
@@ -147,19 +160,8 @@ struct Stager {
   }
   MG_DEVICE void stage(char* lds, int t) const {
     const __amdgpu_buffer_rsrc_t rs = tile_rsrc(base, bytes, step, t);
-    const bool tail = t >= tail_t;
-    const int kl = klim - t * BK;
-    const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int j = swid * PER + i;
-      uint32_t off = voff[i];
-      if (tail) {
-        const int kpos = KC ? ((lane & 7) ^ ((lane >> 3) & 7)) * 8 : 4 * (j & 15) + (lane >> 4);
-        off = kpos < kl ? off : kOOB;
-      }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + j * 1024), 16, off, 0, 0, 0);
-    }
+    for (int i = 0; i < PER; ++i) piece(lds, rs, t, i);
   }
 };
 
@@ -680,6 +682,14 @@ struct W4 {
   static constexpr int NR = 8 + FN;                   // fragment reads / DMA pieces per phase
 };
 
+// the K-loop's final MFMA with the wait states its result needs before any VALU / scratch read
+// (hipcc cannot see the latency of an asm MFMA; whatever it places after the loop -- epilogue reads,
+// spill stores -- must not start inside that window)
+MG_DEVICE void mfma_acc_last(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\ts_nop 7\n\ts_nop 7" : "+a"(acc) : "v"(a), "v"(b) : "memory");
+}
+
+
 template <int BN, bool AK, bool BKC, int EPI, bool OUTF32>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
   static_assert(BN == 256 || BKC, "W4 with BN != 256 needs a k-contiguous B operand");
@@ -761,7 +771,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int i = q / FN, j = q % FN;
-      mfma_acc(acc[i][j], fb1[j], fa1[i]);
+      // every K-tile's final MFMA carries the wait states (a branch on "last K-tile" makes hipcc
+      // duplicate the accumulator into other AGPRs; 16 cycles per 2048 is cheaper than that)
+      if (q == NQ - 1) mfma_acc_last(acc[i][j], fb1[j], fa1[i]);
+      else mfma_acc(acc[i][j], fb1[j], fa1[i]);
       if (q < 2 * NR && (q & 1) == 0) {
         const int r = q >> 1;  // DMA pieces: 8 of A, FN of B
         if (r < 8) sta.piece(dst, ra, tt, r);
@@ -774,7 +787,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
       }
     }
   }
-  asm volatile("s_nop 15\n s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // MFMA results -> readers
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
   epilogue<CF, EPI, OUTF32>(args, acc, m0, n0, wm, wn, wid, lane, smem);
 }
@@ -789,7 +802,8 @@ void launch_w4(GemmArgs a, hipStream_t stream) {
     a.splits = 1;
     a.kchunk = cdiv(a.K, BK) * BK;
     if (OUTF32) set_split(a, 256, 6);
-    const int grid = a.tiles_m * a.tiles_n * a.splits;
+    const int tiles = a.tiles_m * a.tiles_n * a.splits;
+    const int grid = tiles;
     static bool attr_set = false;
     if (!attr_set) {
       hipFuncSetAttribute((const void*)gemm_w4_kernel<BN, AK, BKC, EPI, OUTF32>,

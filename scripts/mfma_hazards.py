@@ -1,0 +1,65 @@
+#!/usr/bin/env python
+"""Flag reads of AGPRs written by an (inline-asm) MFMA too soon after it, in a hipcc .s file.
+
+hipcc does not model the latency of MFMAs issued from inline asm, so a compiler-placed
+v_accvgpr_read / v_accvgpr_mov / scratch_store of the accumulator can read a stale value.
+Counts wait states as issued instructions (s_nop N = N+1) between the MFMA and the reader along
+the straight-line text (branches are ignored: conservative for fall-through code).
+
+    python scripts/mfma_hazards.py file.s [kernel-filter] [--need 12]
+"""
+import re
+import sys
+
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+need = 12
+for a in sys.argv[1:]:
+    if a.startswith("--need="):
+        need = int(a.split("=")[1])
+s = open(args[0]).read()
+filt = args[1] if len(args) > 1 else ""
+
+
+def regs(tok):
+    m = re.match(r"a\[(\d+):(\d+)\]", tok)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.match(r"a(\d+)$", tok)
+    return {int(m.group(1))} if m else set()
+
+
+for m in re.finditer(r"^(_Z\S+):\s*;", s, re.M):
+    name = m.group(1)
+    if filt not in name:
+        continue
+    body = s[m.end():s.find(".Lfunc_end", m.end())].split("\n")
+    last = {}  # agpr -> (line, ws counter at write)
+    ws = 0
+    bad = []
+    for k, line in enumerate(body):
+        t = line.split(";")[0].strip()
+        if not t or t.startswith(".") or t.startswith("#"):
+            continue
+        op = t.split()[0]
+        ops = [o.strip() for o in t[len(op):].split(",")]
+        if op.startswith("s_nop"):
+            ws += int(ops[0]) + 1
+            continue
+        if op.startswith("v_mfma"):
+            for r in regs(ops[0]):
+                last[r] = (k, ws + 1)
+            ws += 4  # issue cycles of the MFMA itself (conservative low)
+            continue
+        reads = set()
+        if op in ("v_accvgpr_read_b32", "v_accvgpr_mov_b32"):
+            reads = regs(ops[1])
+        elif op.startswith("scratch_store") or op.startswith("global_store") or op.startswith("buffer_store"):
+            for o in ops[1:]:
+                reads |= regs(o)
+        for r in reads:
+            if r in last and ws - last[r][1] < need:
+                bad.append((k, r, ws - last[r][1], t))
+        ws += 1
+    print(f"{name[:80]}: {len(bad)} early AGPR reads")
+    for b in bad[:6]:
+        print("   line", b[0], "a%d" % b[1], "ws=%d" % b[2], b[3][:80])
