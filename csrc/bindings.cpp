@@ -246,7 +246,8 @@ void bias_grad(const at::Tensor& dy, const at::Tensor& db) {
 // layout 2 (TN): c[M, N]  += a[K, Ma]^T @ b[K, N]   fp32 c (M <= Ma store rows)
 void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t layout, int64_t epi,
           const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
-          const c10::optional<at::Tensor>& resid, double p, int64_t seed, int64_t M, int64_t N) {
+          const c10::optional<at::Tensor>& resid, double p, int64_t seed, int64_t M, int64_t N,
+          const c10::optional<at::Tensor>& dbias) {
   CHECK_BF16(a); CHECK_BF16(b); CHECK_DEV(c);
   CHECK_CONTIG(a); CHECK_CONTIG(b); CHECK_CONTIG(c);
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm: 2-D operands required");
@@ -292,10 +293,16 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   }
   TORCH_CHECK((size_t)a.numel() * 2 < 0xFFFFFF00u && (size_t)b.numel() * 2 < 0xFFFFFF00u,
               "gemm: operands must be < 4 GiB (32-bit buffer offsets)");
+  float* dbias_p = nullptr;
+  if (dbias.has_value() && dbias->defined()) {
+    CHECK_F32(*dbias);
+    TORCH_CHECK(epi == 4 && dbias->numel() >= N, "gemm: dbias only with the gelu_bwd epilogue");
+    dbias_p = fp(*dbias);
+  }
   DevGuard g(a.device());
   mg::gemm((int)layout, (int)epi, bp(a), bp(b), c.data_ptr(), lda, ldb, ldc, (int)M, (int)N, (int)K,
            (int)a_ext, (int)b_ext, (int)ka, (int)kb, bias_p, aux_p, res_p, (float)p, (uint64_t)seed,
-           cur_stream(), (size_t)a.numel() * 2, (size_t)b.numel() * 2);
+           cur_stream(), (size_t)a.numel() * 2, (size_t)b.numel() * 2, dbias_p);
 }
 
 // ------------------------------------------------------------------------------- attention
@@ -379,7 +386,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attention_set_bwd_variant", &mg::attention_set_bwd_variant);
   m.def("bias_grad", &bias_grad);
   m.def("dropout_bias_grad", &dropout_bias_grad);
-  m.def("gemm", &gemm);
+  m.def("gemm", &gemm, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("layout"), py::arg("epi"),
+        py::arg("bias"), py::arg("aux"), py::arg("resid"), py::arg("p"), py::arg("seed"), py::arg("M"),
+        py::arg("N"), py::arg("dbias") = py::none());
   m.def("gemm_set_variant", &mg::gemm_set_variant);
   m.def("gemm_get_variant", &mg::gemm_get_variant);
   m.def("attention_fwd", &attention_fwd);

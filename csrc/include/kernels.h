@@ -56,7 +56,8 @@ void dropout_bias_grad(const bf16_t* dy, bf16_t* dx, float* db, long M, int N, f
 void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long lda, long ldb,
           long ldc, int M, int N, int K, int a_ext, int b_ext, int ka, int kb, const bf16_t* bias,
           bf16_t* aux, const bf16_t* resid, float p, uint64_t seed, hipStream_t stream,
-          size_t a_bytes, size_t b_bytes);  // operand sizes in bytes (< 4 GiB for the DMA path)
+          size_t a_bytes, size_t b_bytes,  // operand sizes in bytes (< 4 GiB for the DMA path)
+          float* dbias = nullptr);       // EPI 4 only: += column sums of C (bias gradient)
 void gemm_set_variant(int v);  // tile config override: 0 auto (per shape), 1..5 forced (gemm.hip)
 void gemm_set_debug_buffer(unsigned long long* p);  // MG_GEMM_STAMPS diagnostic builds
 int gemm_get_variant();

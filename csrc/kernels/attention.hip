@@ -674,10 +674,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         float p = fexp2(s[r] * a.scale_log2);
-        if (needmask) {
-          const int q = qsub0 + (r & 3) + 8 * (r >> 2) + 4 * h32;
-          if (mykey > q || q >= a.T) p = 0.f;
-        }
+        // select, not a branch (a per-element if became an exec-mask branch per element)
+        const int q = qsub0 + (r & 3) + 8 * (r >> 2) + 4 * h32;
+        const bool kill = needmask & ((mykey > q) | (q >= a.T));  // bitwise: no short-circuit branches
+        p = kill ? 0.f : p;
         float dpv = dp[r], pdrop = p;
         if (a.thr) {
           const float z = (mwr[r] >> mw_bit) & 1u ? a.dscale : 0.f;

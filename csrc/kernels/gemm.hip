@@ -78,6 +78,7 @@ struct GemmArgs {
   int splits, kchunk;         // split-K (fp32-accumulate layout only): K range per split
   uint32_t a_bytes, b_bytes;  // buffer-resource extents (out-of-range reads return 0)
   unsigned long long* dbg;    // MG_GEMM_STAMPS diagnostic builds only: per-wave phase timestamps
+  float* dbias;               // EPI 4: += column sums of the output (the bias gradient), or null
 };
 
 static unsigned long long* g_dbg = nullptr;  // MG_GEMM_STAMPS builds: stamp buffer
@@ -226,6 +227,11 @@ MG_DEVICE void epilogue(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int 
   const int nb = n0 + wn * CF::WTN + (lane >> 4) * 4;
   const bf16_t* __restrict__ bias = args.bias;
   uint2 bs[CF::FN];
+  float csum[EPI == 4 ? CF::FN : 1][4];  // EPI 4 bias gradient: this lane's column partial sums
+#pragma unroll
+  for (int j = 0; j < (EPI == 4 ? CF::FN : 1); ++j)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) csum[j][c] = 0.f;
 #pragma unroll
   for (int j = 0; j < CF::FN; ++j) {
     bs[j] = make_uint2(0u, 0u);
@@ -291,8 +297,38 @@ MG_DEVICE void epilogue(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int 
           v[0] *= bf2f(side[j].x & 0xffffu); v[1] *= bf2f(side[j].x >> 16);
           v[2] *= bf2f(side[j].y & 0xffffu); v[3] *= bf2f(side[j].y >> 16);
         }
-        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(args.C) + off) =
-            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        const uint2 packed = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        if constexpr (EPI == 4) {  // bias gradient of the stored (bf16-rounded) values
+          csum[j][0] += bf2f(packed.x & 0xffffu); csum[j][1] += bf2f(packed.x >> 16);
+          csum[j][2] += bf2f(packed.y & 0xffffu); csum[j][3] += bf2f(packed.y >> 16);
+        }
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(args.C) + off) = packed;
+      }
+    }
+  }
+  if constexpr (EPI == 4) {
+    if (args.dbias) {
+      // sum the 16 rows of each fragment column (lane & 15) by shuffles, the NWM row-waves through
+      // LDS, then one full-width atomic pass over the tile's columns (64 contiguous floats per
+      // wave-instruction: atomics with a few active lanes each run at a small fraction of that)
+      float* cs = reinterpret_cast<float*>(smem);  // [NWM][BN]
+#pragma unroll
+      for (int j = 0; j < CF::FN; ++j)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float t = csum[j][c];
+          t += __shfl_xor(t, 1, 64);
+          t += __shfl_xor(t, 2, 64);
+          t += __shfl_xor(t, 4, 64);
+          t += __shfl_xor(t, 8, 64);
+          if ((lane & 15) == 0) cs[wm * CF::BN + wn * CF::WTN + j * 16 + (lane >> 4) * 4 + c] = t;
+        }
+      __syncthreads();
+      for (int c = threadIdx.x; c < CF::BN; c += CF::NT) {
+        float t = 0.f;
+#pragma unroll
+        for (int r = 0; r < CF::NWM; ++r) t += cs[r * CF::BN + c];
+        if (n0 + c < args.N) atomicAdd(args.dbias + n0 + c, t);
       }
     }
   }
@@ -879,8 +915,9 @@ int gemm_get_variant() { return g_variant; }
 void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long lda, long ldb,
           long ldc, int M, int N, int K, int a_ext, int b_ext, int ka, int kb, const bf16_t* bias,
           bf16_t* aux, const bf16_t* resid, float p, uint64_t seed, hipStream_t stream,
-          size_t a_bytes, size_t b_bytes) {
+          size_t a_bytes, size_t b_bytes, float* dbias) {
   GemmArgs a;
+  a.dbias = dbias;
   a.a_bytes = (uint32_t)std::min<size_t>(a_bytes, 0xFFFFFF00u);
   a.b_bytes = (uint32_t)std::min<size_t>(b_bytes, 0xFFFFFF00u);
   a.A = A; a.B = B; a.C = C; a.lda = lda; a.ldb = ldb; a.ldc = ldc;

@@ -96,7 +96,7 @@ class TransformerBlockFn(torch.autograd.Function):
         G.gemm_tn_acc(dz, u, g[id(wp)][0])
         dpre = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=gd)
         G.gemm_tn_acc(dpre, h2, g[id(wfc)][0])
-        C.bias_grad(dpre, g[id(bfc)][0])
+        C.bias_grad(dpre, g[id(bfc)][0])  # separate pass: cheaper than column sums in the epilogue
         dh2 = G.gemm_dgrad(dpre, wfc)
         dx1 = C.layernorm_bwd(dh2, x1, ln2w, mean2, rstd2, g[id(ln2w)][0], g[id(ln2b)][0], dx2)
         # ---- attention: x1 = x + drop(attn(h Wqkv^T + bqkv) Wo^T + bo)

@@ -30,9 +30,10 @@ def _check2d(t, name):
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: Optional[torch.Tensor] = None,
             epi: str = "none", resid: Optional[torch.Tensor] = None, p: float = 0.0, seed: int = 0,
             pre_out: Optional[torch.Tensor] = None, ld: Optional[int] = None,
-            aux: Optional[torch.Tensor] = None) -> torch.Tensor:
+            aux: Optional[torch.Tensor] = None, dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """C = A @ B^T with a fused epilogue. ``ld`` pads the output row stride (logits).
-    ``gelu`` writes GELU'(z) into ``pre_out``; ``gelu_bwd`` multiplies by ``aux`` (that GELU')."""
+    ``gelu`` writes GELU'(z) into ``pre_out``; ``gelu_bwd`` multiplies by ``aux`` (that GELU') and,
+    with ``dbias`` (fp32 [N]), also adds the output's column sums into it (the bias gradient)."""
     _check2d(a, "A")
     _check2d(b, "B")
     M, K = a.shape
@@ -44,7 +45,7 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: Optional[torch.Tensor] = 
     if code == EPI_BIAS and bias is None:
         code = EPI_NONE
     ext().gemm(a, b, c, 0, code, bias, aux if code == EPI_GELU_BWD else pre_out, resid, float(p),
-               int(seed), M, N)
+               int(seed), M, N, dbias)
     return c
 
 
@@ -55,11 +56,13 @@ def transpose(w: torch.Tensor, ld: Optional[int] = None) -> torch.Tensor:
 
 
 def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, *, epi: str = "none",
-               aux: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """dX = dY @ W (W [N_out, N_in] as stored by nn.Linear), as NT against W^T."""
+               aux: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None,
+               dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dX = dY @ W (W [N_out, N_in] as stored by nn.Linear), as NT against W^T.  With
+    ``epi="gelu_bwd"`` and ``dbias``, the bias gradient of the result is accumulated in the epilogue."""
     if wt is None:
         wt = transpose(w, dy.shape[1])
-    return gemm_nt(dy, wt, epi=epi, aux=aux)
+    return gemm_nt(dy, wt, epi=epi, aux=aux, dbias=dbias)
 
 
 def gemm_nn(a: torch.Tensor, b: torch.Tensor, *, epi: str = "none",

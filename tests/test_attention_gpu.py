@@ -150,3 +150,4 @@ def test_attention_dropout_keep_rate():
     assert (per_head - rate).abs().max().item() < 0.01
     _, _, mask2 = C.attention_fwd(qkv, B, T, H, p, 6)
     assert (keep != _dense_keep(mask2, B, T, H))[..., causal].float().mean().item() > 0.1  # seed matters
+

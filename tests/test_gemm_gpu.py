@@ -119,3 +119,12 @@ def test_dgrad_nt(M, Nout, Nin):
     _check(G.gemm_dgrad(dy, w), ref, Nout)
     gd = _bf(M, Nin, seed=20)
     _check(G.gemm_dgrad(dy, w, epi="gelu_bwd", aux=gd), ref * gd.float(), Nout)
+
+
+def test_dgrad_gelu_bwd_bias_grad():
+    """The GELU' dgrad epilogue also accumulates the output's column sums (fc bias gradient)."""
+    M, Nout, Nin = 1000, 768, 3072
+    dy, w, gd = _bf(M, Nout, seed=21), _bf(Nout, Nin, seed=22), _bf(Nin, seed=23).repeat(M, 1)
+    db = torch.ones(Nin, device=DEV)
+    out = G.gemm_dgrad(dy, w, epi="gelu_bwd", aux=gd.contiguous(), dbias=db)
+    torch.testing.assert_close(db, 1 + out.float().sum(0), atol=5e-1, rtol=1e-2)
