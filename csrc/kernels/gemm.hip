@@ -187,10 +187,174 @@ MG_DEVICE bf16x8 frag(const char* lds, int sb, int ks, int lane) {
   }
 }
 
+// ---- LDS-staged bf16 epilogue.  The fragment layout gives each lane 4 columns of one row, so a
+// direct store is an 8-byte global_store per lane and the store tail of a 256x256 tile is
+// issue-bound (~2x the time of the same bytes in 16-byte stores, guide T21).  Each wave instead
+// writes its finished fragments into its own LDS region (no workgroup barrier: the region is
+// private and a wave's LDS ops complete in order), reads them back as 8 consecutive columns per
+// lane and stores / loads side inputs with 16-byte accesses along whole wave-tile rows.
+// Work that needs the fragment layout (bias, GELU, the row-block dropout mask) runs before the
+// staging; the residual add / GELU' multiply read their side input after it, on fp32 staged values,
+// so the rounding is identical to the direct form.
+constexpr int stage_chf(int fm, int frag_row_bytes, int budget) {
+  int c = fm;
+  while (c > 1 && c * frag_row_bytes > budget) c >>= 1;
+  return c;
+}
+
+MG_DEVICE uint4 load8(const bf16_t* p, int valid) {  // 8 bf16 at p, elements >= valid read as 0
+  if (valid >= 8) return *reinterpret_cast<const uint4*>(p);
+  uint16_t t[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = e < valid ? p[e] : (uint16_t)0;
+  return make_uint4(t[0] | (uint32_t)t[1] << 16, t[2] | (uint32_t)t[3] << 16, t[4] | (uint32_t)t[5] << 16,
+                    t[6] | (uint32_t)t[7] << 16);
+}
+
+MG_DEVICE void store8(bf16_t* p, uint4 v, int valid) {
+  if (valid >= 8) {
+    *reinterpret_cast<uint4*>(p) = v;
+    return;
+  }
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    if (e < valid) p[e] = (uint16_t)(w[e >> 1] >> (16 * (e & 1)));
+}
+
+// LDS -> global half of the staged epilogue for rows [mr, mr + 16 CHF) of the wave tile
+template <class CF, int EPI, bool F32, int S, int CHF, int PR, int IT, bool CHECK>
+MG_DEVICE void staged_rows(const GemmArgs& args, const char* st, const uint4 (&sd)[F32 ? IT : 1], int mr,
+                           int nw, int nlim, int lane) {
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int e = it * 64 + lane, r = e / PR, p = e % PR;
+    const int m = mr + r, n = nw + p * 8;
+    const char* row = st + r * S;
+    uint4 y;
+    if constexpr (F32) {
+      const float4 a = *reinterpret_cast<const float4*>(row + p * 32);
+      const float4 b = *reinterpret_cast<const float4*>(row + p * 32 + 16);
+      float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      const uint32_t w[4] = {sd[it].x, sd[it].y, sd[it].z, sd[it].w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float s = bf2f((w[k >> 1] >> (16 * (k & 1))) & 0xffffu);
+        v[k] = EPI == 3 ? v[k] + s : v[k] * s;
+      }
+      y = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+    } else {
+      y = *reinterpret_cast<const uint4*>(row + p * 16);
+    }
+    const long off = (long)m * args.ldc + n;
+    if constexpr (!CHECK) {
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(args.C) + off) = y;
+      if constexpr (EPI == 2)
+        *reinterpret_cast<uint4*>(args.aux + off) = *reinterpret_cast<const uint4*>(row + CHF * 16 * S + p * 16);
+    } else if (m < args.M && n < nlim) {
+      store8(reinterpret_cast<bf16_t*>(args.C) + off, y, nlim - n);
+      if constexpr (EPI == 2)
+        store8(args.aux + off, *reinterpret_cast<const uint4*>(row + CHF * 16 * S + p * 16), nlim - n);
+    }
+  }
+}
+
+template <class CF, int EPI, int LDSW>
+MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int m0, int n0,
+                               int wm, int wn, int wid, int lane, char* smem) {
+  constexpr bool F32 = EPI == 3 || EPI == 4;     // staged before a bf16 side input is applied
+  constexpr int PL = EPI == 2 ? 2 : 1;           // planes: y (+ GELU' for EPI 2)
+  constexpr int S = CF::WTN * (F32 ? 4 : 2) + 16;  // row stride: rows 4 banks apart (b64/b128 writes)
+  constexpr int CHF = stage_chf(CF::FM, 16 * S * PL, LDSW);  // fragment rows per pass
+  constexpr int PR = CF::WTN / 8;                // 8-column pieces per row
+  constexpr int IT = CHF * 16 * PR / 64;         // pieces per lane per pass
+  static_assert(CHF * 16 * S * PL <= LDSW, "epilogue staging exceeds the wave's LDS share");
+  static_assert((CHF * 16 * PR) % 64 == 0, "pieces must fill whole waves");
+  char* st = smem + wid * LDSW;
+  const int nlim = EPI == 0 ? (int)args.ldc : args.N;
+  const int nw = n0 + wn * CF::WTN;
+  const int nb = nw + (lane >> 4) * 4;
+  const int mw = m0 + wm * CF::WTM;
+  uint2 bs[CF::FN];
+#pragma unroll
+  for (int j = 0; j < CF::FN; ++j) {
+    bs[j] = make_uint2(0u, 0u);
+    if constexpr (EPI == 1 || EPI == 2 || EPI == 3)
+      if (args.bias && nb + j * 16 < nlim) bs[j] = *reinterpret_cast<const uint2*>(args.bias + nb + j * 16);
+  }
+  const bf16_t* __restrict__ side = EPI == 3 ? args.resid : args.aux;
+  const bool full = nw + CF::WTN <= nlim && mw + CF::WTM <= args.M;  // wave-uniform: no per-piece checks
+#pragma unroll
+  for (int c = 0; c < CF::FM / CHF; ++c) {
+    // side inputs of this pass first: their latency hides under the LDS staging
+    uint4 sd[F32 ? IT : 1];
+    if constexpr (F32) {
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int e = it * 64 + lane, r = e / PR, n = nw + (e % PR) * 8;
+        const int m = mw + c * CHF * 16 + r;
+        const bf16_t* p = side + (long)m * args.ldc + n;
+        if (full) sd[it] = *reinterpret_cast<const uint4*>(p);
+        else sd[it] = m < args.M && n < nlim ? load8(p, nlim - n) : make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < CHF; ++ii) {
+      const int i = c * CHF + ii;
+      const int m = mw + i * 16 + (lane & 15);
+      char* row = st + (ii * 16 + (lane & 15)) * S;
+      uint4 rnd = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int j = 0; j < CF::FN; ++j) {
+        const int n = nb + j * 16;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if constexpr (EPI == 1 || EPI == 2 || EPI == 3) {
+          v[0] += bf2f(bs[j].x & 0xffffu); v[1] += bf2f(bs[j].x >> 16);
+          v[2] += bf2f(bs[j].y & 0xffffu); v[3] += bf2f(bs[j].y >> 16);
+        }
+        const int col = j * 16 + (lane >> 4) * 4;
+        if constexpr (EPI == 2) {  // y = GELU(z); GELU'(z) into the second plane
+          float gd[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float sg = gelu_sigmoid(v[r]);
+            gd[r] = gelu_grad_from(v[r], sg);
+            v[r] *= sg;
+          }
+          *reinterpret_cast<uint2*>(row + CHF * 16 * S + col * 2) =
+              make_uint2(pack2(gd[0], gd[1]), pack2(gd[2], gd[3]));
+        }
+        if constexpr (EPI == 3) {
+          if (args.thr) {  // one Philox call per 64-column block of this lane's row (common.h rowdrop)
+            const int w16 = (n >> 4) & 3;
+            if (CF::WTN % 64 == 0 ? (j & 3) == 0 : (j == 0 || w16 == 0)) rnd = rowdrop_call(args.seed, m, n, args.N);
+            rowdrop4(v, word_of(rnd, CF::WTN % 64 == 0 ? (j & 3) : w16), args.thr, args.scale);
+          }
+        }
+        if constexpr (F32)
+          *reinterpret_cast<float4*>(row + col * 4) = make_float4(v[0], v[1], v[2], v[3]);
+        else
+          *reinterpret_cast<uint2*>(row + col * 2) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (full) staged_rows<CF, EPI, F32, S, CHF, PR, IT, false>(args, st, sd, mw + c * CHF * 16, nw, nlim, lane);
+    else staged_rows<CF, EPI, F32, S, CHF, PR, IT, true>(args, st, sd, mw + c * CHF * 16, nw, nlim, lane);
+    asm volatile("" ::: "memory");  // the next pass's LDS writes stay behind these reads
+  }
+}
+
 // Shared epilogue: lane holds acc[i][j] = C[m0+wm*WTM+16i+(lane&15)][n0+wn*WTN+16j+4(lane>>4) .. +3].
-template <class CF, int EPI, bool OUTF32>
+// LDSW: LDS bytes each wave may use for the staged form (the K-loop's buffers are free by then).
+template <class CF, int EPI, bool OUTF32, int LDSW>
 MG_DEVICE void epilogue(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int m0, int n0, int wm,
                         int wn, int wid, int lane, char* smem) {
+  if constexpr (!OUTF32) {
+    if (EPI != 4 || !args.dbias) {
+      epilogue_staged<CF, EPI, LDSW>(args, acc, m0, n0, wm, wn, wid, lane, smem);
+      return;
+    }
+  }
   if constexpr (OUTF32) {
     if (args.splits > 1) {
       // split-K: fp32 atomics into C.  Each wave stages its tile through LDS 32 rows at a time
@@ -418,7 +582,7 @@ __global__ __launch_bounds__(CF::NT, 2) void gemm_kernel(const GemmArgs args) {
     __builtin_amdgcn_s_barrier();
   }
 
-  epilogue<CF, EPI, OUTF32>(args, acc, m0, n0, wm, wn, wid, lane, smem);
+  epilogue<CF, EPI, OUTF32, CF::SMEM / CF::NW>(args, acc, m0, n0, wm, wn, wid, lane, smem);
 }
 
 // ============================================================================================
@@ -642,7 +806,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const GemmArgs args) {
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // sink DMA of the tail
   __syncthreads();
-  epilogue<CF, EPI, OUTF32>(args, acc, m0, n0, wr, wc, wid, lane, smem);
+  epilogue<CF, EPI, OUTF32, ppk::SMEM / 8>(args, acc, m0, n0, wr, wc, wid, lane, smem);
 }
 
 // Split-K for the fp32-accumulate (weight-gradient) layout: pick the split that minimises
@@ -825,7 +989,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  epilogue<CF, EPI, OUTF32>(args, acc, m0, n0, wm, wn, wid, lane, smem);
+  epilogue<CF, EPI, OUTF32, WK::SMEM / 4>(args, acc, m0, n0, wm, wn, wid, lane, smem);
 }
 
 template <int BN, bool AK, bool BKC, int EPI, bool OUTF32>
