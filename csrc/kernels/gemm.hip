@@ -166,6 +166,27 @@ struct Stager {
   }
 };
 
+// ---- transposing LDS read as inline asm.  Through the builtin, hipcc's wait-count pass sees an LDS
+// read it cannot disambiguate from the in-flight LDS-DMA writes and puts s_waitcnt vmcnt(0) in
+// front of it, which drains the DMA pipeline on every K-step of an m/n-contiguous operand (a third
+// of the throughput).  The asm form is invisible to that pass, so every consumer makes the results
+// valid itself: lds_ready() = s_waitcnt lgkmcnt(0) + a register tie, so no use (or copy) of a
+// fragment is scheduled above the wait (scripts/mfma_hazards.py --lds checks the compiled code).
+MG_DEVICE uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+MG_DEVICE s16x4 ds_read_tr16(const char* p) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_addr(p)));
+  return r;
+}
+template <int N>
+MG_DEVICE void lds_ready(bf16x8 (&f)[N], bool wait = true) {
+  if (wait) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(f[i]));
+}
+
 // ---- fragment read for 16-wide subtile sb, k-step ks (32 k)
 template <bool KC>
 MG_DEVICE bf16x8 frag(const char* lds, int sb, int ks, int lane) {
@@ -180,8 +201,8 @@ MG_DEVICE bf16x8 frag(const char* lds, int sb, int ks, int lane) {
     const int r0 = ks * 32 + 8 * g + q, r1 = r0 + 4;
     const char* a0 = img + r0 * 256 + ((chk ^ swz_mn(r0)) << 4) + (p & 1) * 8;
     const char* a1 = img + r1 * 256 + ((chk ^ swz_mn(r1)) << 4) + (p & 1) * 8;
-    const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
-    const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+    const s16x4 x = ds_read_tr16(a0);
+    const s16x4 y = ds_read_tr16(a1);
     const s16x8 v = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
     return __builtin_bit_cast(bf16x8, v);
   }
@@ -563,6 +584,10 @@ __global__ __launch_bounds__(CF::NT, 2) void gemm_kernel(const GemmArgs args) {
       for (int i = 0; i < CF::FM; ++i) fa[i] = frag<AK>(sa, wm * CF::FM + i, ks, lane);
 #pragma unroll
       for (int j = 0; j < CF::FN; ++j) fb[j] = frag<BKC>(sb, wn * CF::FN + j, ks, lane);
+      if constexpr (!AK || !BKC) {
+        lds_ready(fa);
+        lds_ready(fb, false);
+      }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < CF::FM; ++i)
@@ -781,7 +806,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const GemmArgs args) {
       PP_STAMP(p, 2);
       __builtin_amdgcn_s_barrier();
       PP_STAMP(p, 3);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      lds_ready(fa);
+      lds_ready(fb, false);
       __builtin_amdgcn_sched_barrier(0);
       PP_STAMP(p, 4);
       __builtin_amdgcn_s_setprio(1);
@@ -939,9 +965,11 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
 
   bf16x8 fa0[8], fb0[FN], fa1[8], fb1[FN];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) fa0[i] = frag<AK>(smem, wm * 8 + i, 0, lane);
-#pragma unroll
   for (int j = 0; j < FN; ++j) fb0[j] = frag<BKC>(smem + CF::A_BYTES, wn * FN + j, 0, lane);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) fa0[i] = frag<AK>(smem, wm * 8 + i, 0, lane);
+  lds_ready(fa0);
+  lds_ready(fb0, false);
 
   for (int kt = 0; kt < nk; ++kt) {
     const char* sa = smem + (kt & 1) * WK::STAGE;
@@ -951,13 +979,16 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
       const int i = q / FN, j = q % FN;
       mfma_acc(acc[i][j], fb0[j], fa0[i]);
       if ((q & 1) == 0 && q < 2 * NR) {
-        const int r = q >> 1;  // A fragments then B fragments
-        if (r < 8) fa1[r] = frag<AK>(sa, wm * 8 + r, 1, lane);
-        else fb1[r - 8] = frag<BKC>(sa + CF::A_BYTES, wn * FN + r - 8, 1, lane);
+        // B fragments first: the next phase's first FN MFMAs use fa[0] with every fb[j]
+        const int r = q >> 1;
+        if (r < FN) fb1[r] = frag<BKC>(sa + CF::A_BYTES, wn * FN + r, 1, lane);
+        else fa1[r - FN] = frag<AK>(sa, wm * 8 + r - FN, 1, lane);
       }
     }
     // tile kt+1 landed (this wave's DMA), every wave done reading buffer kt & 1
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    lds_ready(fa1, false);
+    lds_ready(fb1, false);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     // phase B: k32 step 1 of tile kt; DMA of tile kt+2 into buffer kt & 1 (or the sink) and the
@@ -967,7 +998,6 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
     char* dst = t2 < nk ? smem + (kt & 1) * WK::STAGE : smem + WK::SINK;
     const __amdgpu_buffer_rsrc_t ra = sta.rsrc(tt), rb = stb.rsrc(tt);
     const char* sn = smem + ((kt + 1) & 1) * WK::STAGE;
-    constexpr int QR = NQ - 2 * NR;  // fragment reads in the odd slots of the last 2*NR MFMAs
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int i = q / FN, j = q % FN;
@@ -980,12 +1010,16 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
         if (r < 8) sta.piece(dst, ra, tt, r);
         else stb.piece(t2 < nk ? dst + CF::A_BYTES : dst, rb, tt, r - 8);
       }
-      if (q >= QR && ((q - QR) & 1) == 1) {
-        const int r = (q - QR) >> 1;  // fragment reads of tile kt+1 step 0
-        if (r < 8) fa0[r] = frag<AK>(sn, wm * 8 + r, 0, lane);
-        else fb0[r - 8] = frag<BKC>(sn + CF::A_BYTES, wn * FN + r - 8, 0, lane);
+      if (q < 2 * NR && (q & 1) == 1) {
+        // fragment reads of tile kt+1 step 0, B first, interleaved with the DMA pieces early in the
+        // phase so they have ~3/4 of it to land before the next phase A needs them
+        const int r = q >> 1;
+        if (r < FN) fb0[r] = frag<BKC>(sn + CF::A_BYTES, wn * FN + r, 0, lane);
+        else fa0[r - FN] = frag<AK>(sn, wm * 8 + r - FN, 0, lane);
       }
     }
+    lds_ready(fa0);  // read early in phase B: long landed, the wait is free
+    lds_ready(fb0, false);
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1051,7 +1085,7 @@ int pick_config(int M, int N, int K, int layout) {
     return r192 * 108 < r256 * 100 ? 6 : 5;
   }
   if (layout == 1) return (K >= 1536 || t256 >= 1024) ? 4 : 1;
-  return (long)M * N >= (1L << 20) ? 4 : 1;
+  return (long)M * N >= (1L << 20) ? 5 : 1;  // wgrad: W4 since the asm tr reads (bench_wgrad.py)
 }
 
 template <bool AK, bool BKC, int EPI, bool OUTF32>

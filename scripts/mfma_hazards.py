@@ -63,3 +63,48 @@ for m in re.finditer(r"^(_Z\S+):\s*;", s, re.M):
     print(f"{name[:80]}: {len(bad)} early AGPR reads")
     for b in bad[:6]:
         print("   line", b[0], "a%d" % b[1], "ws=%d" % b[2], b[3][:80])
+
+
+# ---- --lds: registers written by inline-asm LDS reads (ds_read_b64_tr_b16, invisible to hipcc's
+# wait-count pass) must not be read before an s_waitcnt lgkmcnt(0) retires them (gemm.hip lds_ready).
+def vregs(tok):
+    m = re.match(r"v\[(\d+):(\d+)\]", tok)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.match(r"v(\d+)$", tok)
+    return {int(m.group(1))} if m else set()
+
+
+if "--lds" in sys.argv:
+    for m in re.finditer(r"^(_Z\S+):\s*;", s, re.M):
+        name = m.group(1)
+        if filt not in name:
+            continue
+        body = s[m.end():s.find(".Lfunc_end", m.end())].split("\n")
+        pending = set()
+        bad = []
+        for k, line in enumerate(body):
+            t = line.split(";")[0].strip()
+            if not t or t.startswith(".") or t.startswith("#"):
+                continue
+            op = t.split()[0]
+            ops = [o.strip() for o in t[len(op):].split(",")]
+            if op == "s_waitcnt" and "lgkmcnt(0)" in t:
+                pending.clear()
+                continue
+            if op == "ds_read_b64_tr_b16":
+                srcs = vregs(ops[1].split()[0])
+                if srcs & pending:
+                    bad.append((k, t))
+                pending |= vregs(ops[0])
+                continue
+            # every operand of any other instruction counts as a read (conservative; a plain
+            # overwrite of a pending register is a WAW hazard too)
+            used = set()
+            for o in ops:
+                used |= vregs(o.split()[0]) if o else set()
+            if used & pending:
+                bad.append((k, t))
+        print(f"{name[:80]}: {len(bad)} early reads of asm LDS results")
+        for b in bad[:6]:
+            print("   line", b[0], b[1][:90])

@@ -25,3 +25,20 @@ def test_gemm_inline_asm_mfma_hazards(tmp_path):
     assert lines, r.stdout
     bad = [l for l in lines if not l.rstrip().endswith(": 0 early AGPR reads")]
     assert not bad, "\n".join(bad)
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_gemm_asm_lds_reads_waited(tmp_path):
+    """Transposing LDS reads are inline asm (so hipcc does not drain the LDS-DMA queue before each
+    one); no instruction may read their destination registers before an lgkmcnt(0)."""
+    out = tmp_path / "gemm.s"
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=fast",
+                    "--cuda-device-only", "-S", "-I" + os.path.join(ROOT, "csrc", "include"),
+                    os.path.join(ROOT, "csrc", "kernels", "gemm.hip"), "-o", str(out)],
+                   check=True, capture_output=True)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "mfma_hazards.py"), str(out), "gemm", "--lds"],
+                       check=True, capture_output=True, text=True)
+    lines = [l for l in r.stdout.splitlines() if "asm LDS results" in l]
+    assert len(lines) > 10, r.stdout
+    bad = [l for l in lines if not l.rstrip().endswith(": 0 early reads of asm LDS results")]
+    assert not bad, "\n".join(bad)
