@@ -337,7 +337,7 @@ at::Tensor attention_bwd(const at::Tensor& qkv, const at::Tensor& out, const at:
   auto dqkv = at::empty_like(qkv);
   auto opts = qkv.options().dtype(at::kFloat);
   auto delta = at::empty({B * H * T}, opts);
-  auto dq = at::empty({B * T * D}, opts);
+  auto dq = at::empty({mg::attention_bwd_keyblocks((int)T) * B * T * D}, opts);  // dQ partials
   const uint32_t* mp = nullptr;
   if (p > 0) {
     CHECK_DEV(mask);

@@ -68,7 +68,9 @@ size_t attention_dropout_mask_words(int B, int T, int H);
 void attention_set_bwd_variant(int v);  // 0 auto (256-key blocks), 1 force 128-key blocks
 void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, uint32_t* dmask, int B, int T, int H,
                    int hd, float p, uint64_t seed, hipStream_t stream);
-// delta [B*H*T] and dq [B*T*D] fp32 are workspaces; writes all three slots of dqkv
+// delta [B*H*T] and dq [attention_bwd_keyblocks(T) * B*T*D] fp32 are workspaces; writes all three
+// slots of dqkv
+int attention_bwd_keyblocks(int T);
 void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse,
                    const uint32_t* dmask, float* delta, float* dq, bf16_t* dqkv, int B, int T, int H,
                    int hd, float p, uint64_t seed, hipStream_t stream);

@@ -55,7 +55,8 @@ struct AttnArgs {
   float* lse;          // [B*H*T], log2 domain
   const bf16_t* dout;  // bwd
   const float* delta;  // bwd [B*H*T]
-  float* dq;           // bwd [B*T, D] fp32 accumulator
+  float* dq;           // bwd fp32 dQ: [B*T, D] atomic accumulator, or per-key-block partials
+  long dq_part;        // bwd256: elements between key-block partials of dq (plain stores)
   bf16_t* dqkv;        // bwd [B*T, 3D]
   uint32_t* dmask;     // dropout keep-bits [B*H*T][2*ceil(T/64)] (fwd writes, bwd reads)
   int B, T, H, hd, D;
@@ -550,6 +551,31 @@ MG_DEVICE void store_rows(char* lds, const uint4 (&reg)[ROWS * 8 / NT]) {
   }
 }
 
+// In place on one 32x32 (query rows x key lanes) tile: s <- dropped P (dV operand),
+// dp <- dS = P * (dP~ * Z - delta).  Row r of the lane is query q0 + (r & 3) + 8 (r >> 2).
+template <bool MASK>
+MG_DEVICE void bwd_softmax_grad(f32x16& s, f32x16& dp, const float (&dl)[16], const uint32_t (&mwr)[16],
+                                const AttnArgs& a, int mykey, int mw_bit, int q0) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float p = fexp2(s[r] * a.scale_log2);
+    if constexpr (MASK) {
+      // select, not a branch (a per-element if became an exec-mask branch per element)
+      const int q = q0 + (r & 3) + 8 * (r >> 2);
+      const bool kill = (mykey > q) | (q >= a.T);  // bitwise: no short-circuit branches
+      p = kill ? 0.f : p;
+    }
+    float dpv = dp[r], pdrop = p;
+    if (a.thr) {
+      const float z = (mwr[r] >> mw_bit) & 1u ? a.dscale : 0.f;
+      pdrop = p * z;
+      dpv *= z;
+    }
+    s[r] = pdrop;
+    dp[r] = p * (dpv - dl[r]);
+  }
+}
+
 template <int NKS>
 __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -606,7 +632,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
     const int t = threadIdx.x;
     if (t < 2 * BQ) {
       const int q = qt * BQ + (t & (BQ - 1));
-      rl = q < a.T ? (t < BQ ? lseg[q] * inv_c : dlg[q]) : 0.f;
+      rl = q < a.T ? (t < BQ ? -lseg[q] * inv_c : dlg[q]) : 0.f;  // -lse/c: the S init
     }
     if (a.thr) {  // word j of query row q -> sMW[j * 64 + q]
       const int q = qt * BQ + (t & 63), j = t >> 6;
@@ -652,7 +678,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
         const int q4 = qs * 32 + 8 * g + 4 * h32;
         const float4 x = *reinterpret_cast<const float4*>(sL + q4);
         const float4 y = *reinterpret_cast<const float4*>(sL + BQ + q4);
-        lr[4 * g] = -x.x; lr[4 * g + 1] = -x.y; lr[4 * g + 2] = -x.z; lr[4 * g + 3] = -x.w;
+        lr[4 * g] = x.x; lr[4 * g + 1] = x.y; lr[4 * g + 2] = x.z; lr[4 * g + 3] = x.w;
         dl[4 * g] = y.x; dl[4 * g + 1] = y.y; dl[4 * g + 2] = y.z; dl[4 * g + 3] = y.w;
         if (a.thr) {
           const uint4 m4 = *reinterpret_cast<const uint4*>(sMW + mw_col * 64 + q4);
@@ -670,23 +696,11 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
       }
       // rows = queries qs*32 + (r&3) + 8(r>>2) + 4*h32 ; col = key (lane).  In place:
       // s <- dropped P (dV operand), dp <- dS = P * (dP~ * Z - delta).
-      const bool needmask = wave_kmin + 31 > qsub0 || qsub0 + 31 >= a.T;  // wave-uniform
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float p = fexp2(s[r] * a.scale_log2);
-        // select, not a branch (a per-element if became an exec-mask branch per element)
-        const int q = qsub0 + (r & 3) + 8 * (r >> 2) + 4 * h32;
-        const bool kill = needmask & ((mykey > q) | (q >= a.T));  // bitwise: no short-circuit branches
-        p = kill ? 0.f : p;
-        float dpv = dp[r], pdrop = p;
-        if (a.thr) {
-          const float z = (mwr[r] >> mw_bit) & 1u ? a.dscale : 0.f;
-          pdrop = p * z;
-          dpv *= z;
-        }
-        s[r] = pdrop;
-        dp[r] = p * (dpv - dl[r]);
-      }
+      // wave-uniform: only diagonal / past-T tiles pay for the causal mask
+      if (wave_kmin + 31 > qsub0 || qsub0 + 31 >= a.T)
+        bwd_softmax_grad<true>(s, dp, dl, mwr, a, mykey, mw_bit, qsub0 + 4 * h32);
+      else
+        bwd_softmax_grad<false>(s, dp, dl, mwr, a, mykey, mw_bit, qsub0 + 4 * h32);
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         const bf16x8 pf = pack_frag(s, st);
@@ -740,13 +754,15 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
           dq[4 * g] += x[0]; dq[4 * g + 1] += x[1]; dq[4 * g + 2] += x[2]; dq[4 * g + 3] += x[3];
         }
       }
+      // this key block's partial: plain stores (rows q >= kb0 are all written by this workgroup;
+      // attn_dq_finalize sums the partials of key blocks kb0 <= q), no atomics, no memset
       const int d = dblk * 32 + l32;
       if (d < a.hd) {
-        float* dqb = a.dq + ((long)b * a.T) * a.D + hh * a.hd + d;
+        float* dqb = a.dq + kb * a.dq_part + ((long)b * a.T) * a.D + hh * a.hd + d;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int q = qbase + qs * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
-          if (q < a.T) atomicAdd(dqb + (long)q * a.D, dq[r]);
+          if (q < a.T) dqb[(long)q * a.D] = dq[r];
         }
       }
     }
@@ -778,17 +794,24 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
   }
 }
 
-// dqkv Q slot = bf16(dq * scale)
+// dqkv Q slot = bf16(scale * sum of the dQ partials).  part = 0: one atomic accumulator;
+// otherwise partial kb (stride part) holds key block kb's contribution for rows t >= kb * KB2.
 __global__ __launch_bounds__(256) void attn_dq_finalize_kernel(const float* __restrict__ dq,
                                                                bf16_t* __restrict__ dqkv, long rows,
-                                                               int D, float sc) {
+                                                               int D, int T, long part, float sc) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;  // over rows * D/8
   const long n8 = rows * (D / 8);
   if (i >= n8) return;
   const long r = i / (D / 8);
   const int c = (int)(i % (D / 8)) * 8;
-  const float4 x0 = *reinterpret_cast<const float4*>(dq + r * D + c);
-  const float4 x1 = *reinterpret_cast<const float4*>(dq + r * D + c + 4);
+  const int np = part ? (int)(r % T) / KB2 + 1 : 1;
+  float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
+  for (int k = 0; k < np; ++k) {
+    const float* src = dq + k * part + r * D + c;
+    const float4 y0 = *reinterpret_cast<const float4*>(src), y1 = *reinterpret_cast<const float4*>(src + 4);
+    x0.x += y0.x; x0.y += y0.y; x0.z += y0.z; x0.w += y0.w;
+    x1.x += y1.x; x1.y += y1.y; x1.z += y1.z; x1.w += y1.w;
+  }
   const float f[8] = {x0.x * sc, x0.y * sc, x0.z * sc, x0.w * sc, x1.x * sc, x1.y * sc, x1.z * sc, x1.w * sc};
   st16(dqkv + r * 3L * D + c, pack8(f));
 }
@@ -892,6 +915,9 @@ static AttnArgs make_args(int B, int T, int H, int hd, float p, uint64_t seed) {
 
 void attention_set_bwd_variant(int v) { g_attn_bwd_variant = v; }
 
+// number of dQ partial buffers attention_bwd needs (the 256-key kernel writes one per key block)
+int attention_bwd_keyblocks(int T) { return (g_attn_bwd_variant != 1 && T > 128) ? cdiv(T, KB2) : 1; }
+
 size_t attention_dropout_mask_words(int B, int T, int H) {
   return (size_t)B * H * T * 2 * ((T + 63) / 64);
 }
@@ -916,8 +942,10 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
   if (a.thr && !dmask) a.thr = 0;
   const long nchunks = (long)B * T * H * hd / 8;
   attn_bwd_pre_kernel<<<cdiv(nchunks, 256), 256, 0, stream>>>(dout, out, delta, B, T, H, hd, H * hd);
-  hipMemsetAsync(dq, 0, sizeof(float) * (size_t)B * T * H * hd, stream);
-  if (g_attn_bwd_variant != 1 && T > 128) {  // 256-key blocks (half the dQ atomics)
+  const bool blk256 = g_attn_bwd_variant != 1 && T > 128;
+  a.dq_part = blk256 ? (long)B * T * H * hd : 0;
+  if (!blk256) hipMemsetAsync(dq, 0, sizeof(float) * (size_t)B * T * H * hd, stream);
+  if (blk256) {  // 256-key blocks, dQ partials per key block
     static bool attr = false;
     if (!attr) {
       hipFuncSetAttribute((const void*)attn_bwd256_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, B2_SMEM);
@@ -936,8 +964,8 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
     else attn_bwd_kernel<1><<<grid, 256, BWD_SMEM, stream>>>(a);
   }
   const long n8 = (long)B * T * (H * hd / 8);
-  attn_dq_finalize_kernel<<<cdiv(n8, 256), 256, 0, stream>>>(dq, dqkv, (long)B * T, H * hd,
-                                                             1.f / sqrtf((float)hd));
+  attn_dq_finalize_kernel<<<cdiv(n8, 256), 256, 0, stream>>>(dq, dqkv, (long)B * T, H * hd, T,
+                                                             a.dq_part, 1.f / sqrtf((float)hd));
 }
 
 }  // namespace mg
