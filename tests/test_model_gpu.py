@@ -17,8 +17,8 @@ def _cfg(**kw):
     return GPTConfig(**base)
 
 
-@pytest.mark.parametrize("hd", [64, 32])
-def test_forward_backward_matches_reference(hd):
+@pytest.mark.parametrize("hd,gs", [(64, 1.0), (32, 1.0), (64, 0.25)])
+def test_forward_backward_matches_reference(hd, gs):
     torch.manual_seed(0)
     cpu = GPT(_cfg(n_head=128 // hd), verbose=False)
     gpu = copy.deepcopy(cpu).cuda().to(torch.bfloat16)
@@ -34,8 +34,8 @@ def test_forward_backward_matches_reference(hd):
     assert lg.shape == lc.shape
     torch.testing.assert_close(lg.float().cpu(), lc.detach(), atol=6e-2, rtol=5e-2)
     assert abs(loss_g.item() - loss_c.item()) < 2e-2
-    loss_c.backward()
-    loss_g.backward()
+    (loss_c * gs).backward()  # gs != 1: the upstream gradient reaches the fused loss backward
+    (loss_g * gs).backward()
     for (n, pc), pg in zip(cpu.named_parameters(), gpu.parameters()):
         gc, gg = pc.grad, pg.grad.float().cpu()
         scale = gc.abs().max().item() + 1e-8
