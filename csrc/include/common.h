@@ -21,6 +21,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
 MG_DEVICE float bf2f(uint32_t v) { return __uint_as_float(v << 16); }
 
@@ -29,8 +31,10 @@ MG_DEVICE bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, h);
 }
 
+// ONE v_cvt_pk_bf16_f32 (two scalar converts + shift + or when written element-wise)
 MG_DEVICE uint32_t pack2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  const f32x2 v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
 // 8 x bf16 <-> 8 x f32 through one 16-byte vector.

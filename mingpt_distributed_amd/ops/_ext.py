@@ -6,6 +6,7 @@ silent eager fallback for a GPU tensor.  CPU tensors never reach the extension.
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
 
 _EXT = None
@@ -19,7 +20,13 @@ def _load():
     try:
         import torch  # noqa: F401  (loads torch's HIP runtime first; _C.so binds to it)
 
-        _EXT = importlib.import_module("mingpt_distributed_amd._C")
+        alt = os.environ.get("MINGPT_EXT_SO")  # A/B runs: another build of the same extension
+        if alt:
+            spec = importlib.util.spec_from_file_location("mingpt_distributed_amd._C", alt)
+            _EXT = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_EXT)
+        else:
+            _EXT = importlib.import_module("mingpt_distributed_amd._C")
     except Exception as e:  # pragma: no cover - depends on build state
         _ERR = e
 
