@@ -576,6 +576,29 @@ MG_DEVICE void bwd_softmax_grad(f32x16& s, f32x16& dp, const float (&dl)[16], co
   }
 }
 
+// bwd256 form: K is pre-scaled by c in LDS, so S' = Q (cK)^T - lse arrives in the log2 domain and
+// p = exp2(S') needs no multiply.  Dropout keeps/zeroes with a sign-extended bit field (v_bfe_i32
+// + v_and, no compare/select) and its 1/(1-p) is folded: into dS through one FMA, into dV at the
+// store.  dS = P * (Z dP~ / (1-p) - delta); s <- Z P (dV operand, unscaled).
+template <bool MASK>
+MG_DEVICE void bwd_softmax_grad2(f32x16& s, f32x16& dp, const float (&dl)[16], const uint32_t (&mwr)[16],
+                                 const AttnArgs& a, int mykey, int mw_bit, int q0) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float p = fexp2(s[r]);
+    if constexpr (MASK) {
+      const int q = q0 + (r & 3) + 8 * (r >> 2);
+      const bool kill = (mykey > q) | (q >= a.T);
+      p = kill ? 0.f : p;
+    }
+    // no dropout: every keep word is all ones (set when staged), dscale = 1
+    const int keep = __builtin_amdgcn_sbfe((int)mwr[r], mw_bit, 1);  // 0 or -1
+    s[r] = __int_as_float(__float_as_int(p) & keep);
+    const float dpv = __int_as_float(__float_as_int(dp[r]) & keep);
+    dp[r] = p * __builtin_fmaf(dpv, a.dscale, -dl[r]);
+  }
+}
+
 template <int NKS>
 __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -595,7 +618,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
   char* sdS = smem + B2_DS;
   const float* sL = reinterpret_cast<const float*>(smem + B2_L);
   const uint32_t* sMW = reinterpret_cast<const uint32_t*>(smem + B2_MW);
-  const float inv_c = 1.f / a.scale_log2;
 
   int mykey, wave_kmin;
   bf16x8 vf[4];
@@ -605,6 +627,14 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
     wave_kmin = kb0 + 32 * w;
     uint4 rk[4];
     load_rows<KB2, 512>(rk, Kg, ld, kb0, a.T, a.hd);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // K <- c K (see bwd_softmax_grad2); dQ is rescaled by ln 2
+      float f[8];
+      unpack8(rk[i], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= a.scale_log2;
+      rk[i] = pack8(f);
+    }
     store_rows<KB2, 512>(sK, rk);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -625,14 +655,14 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
 
   uint4 rq[1], rd[1];
   float rl = 0.f;
-  uint32_t rmw = 0;
+  uint32_t rmw = 0xffffffffu;  // no dropout: every key kept
   auto issue = [&](int qt) {
     load_rows<BQ, 512>(rq, Qg, ld, qt * BQ, a.T, a.hd);
     load_rows<BQ, 512>(rd, dOg, a.D, qt * BQ, a.T, a.hd);
     const int t = threadIdx.x;
     if (t < 2 * BQ) {
       const int q = qt * BQ + (t & (BQ - 1));
-      rl = q < a.T ? (t < BQ ? -lseg[q] * inv_c : dlg[q]) : 0.f;  // -lse/c: the S init
+      rl = q < a.T ? (t < BQ ? -lseg[q] : dlg[q]) : 0.f;  // -lse: the S init (K holds c K)
     }
     if (a.thr) {  // word j of query row q -> sMW[j * 64 + q]
       const int q = qt * BQ + (t & 63), j = t >> 6;
@@ -643,7 +673,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
     store_rows<BQ, 512>(smem + B2_Q, rq);
     store_rows<BQ, 512>(smem + B2_DO, rd);
     if (threadIdx.x < 2 * BQ) reinterpret_cast<float*>(smem + B2_L)[threadIdx.x] = rl;
-    if (a.thr) reinterpret_cast<uint32_t*>(smem + B2_MW)[threadIdx.x] = rmw;
+    reinterpret_cast<uint32_t*>(smem + B2_MW)[threadIdx.x] = rmw;
   };
   issue(qt0);
   commit();
@@ -680,7 +710,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
         const float4 y = *reinterpret_cast<const float4*>(sL + BQ + q4);
         lr[4 * g] = x.x; lr[4 * g + 1] = x.y; lr[4 * g + 2] = x.z; lr[4 * g + 3] = x.w;
         dl[4 * g] = y.x; dl[4 * g + 1] = y.y; dl[4 * g + 2] = y.z; dl[4 * g + 3] = y.w;
-        if (a.thr) {
+        {
           const uint4 m4 = *reinterpret_cast<const uint4*>(sMW + mw_col * 64 + q4);
           mwr[4 * g] = m4.x; mwr[4 * g + 1] = m4.y; mwr[4 * g + 2] = m4.z; mwr[4 * g + 3] = m4.w;
         }
@@ -698,9 +728,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
       // s <- dropped P (dV operand), dp <- dS = P * (dP~ * Z - delta).
       // wave-uniform: only diagonal / past-T tiles pay for the causal mask
       if (wave_kmin + 31 > qsub0 || qsub0 + 31 >= a.T)
-        bwd_softmax_grad<true>(s, dp, dl, mwr, a, mykey, mw_bit, qsub0 + 4 * h32);
+        bwd_softmax_grad2<true>(s, dp, dl, mwr, a, mykey, mw_bit, qsub0 + 4 * h32);
       else
-        bwd_softmax_grad<false>(s, dp, dl, mwr, a, mykey, mw_bit, qsub0 + 4 * h32);
+        bwd_softmax_grad2<false>(s, dp, dl, mwr, a, mykey, mw_bit, qsub0 + 4 * h32);
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         const bf16x8 pf = pack_frag(s, st);
@@ -773,6 +803,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
   const int lane = threadIdx.x & 63, h32 = lane >> 5;
   if (mykey < a.T) {
     const float sc = a.scale_log2 * 0.6931471805599453f;  // 1/sqrt(hd)
+    const float vs = a.thr ? a.dscale : 1.f;                // dropout keep scale, folded (see above)
     bf16_t* krow = a.dqkv + ((long)b * a.T + mykey) * ld + a.D + hh * a.hd;
     bf16_t* vrow = krow + a.D;
 #pragma unroll
@@ -781,14 +812,14 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
       if (d < a.hd) {
         *reinterpret_cast<uint2*>(krow + d) = make_uint2(pack2(dk0[4 * g] * sc, dk0[4 * g + 1] * sc),
                                                          pack2(dk0[4 * g + 2] * sc, dk0[4 * g + 3] * sc));
-        *reinterpret_cast<uint2*>(vrow + d) = make_uint2(pack2(dv0[4 * g], dv0[4 * g + 1]),
-                                                         pack2(dv0[4 * g + 2], dv0[4 * g + 3]));
+        *reinterpret_cast<uint2*>(vrow + d) = make_uint2(pack2(dv0[4 * g] * vs, dv0[4 * g + 1] * vs),
+                                                         pack2(dv0[4 * g + 2] * vs, dv0[4 * g + 3] * vs));
       }
       if (32 + d < a.hd) {
         *reinterpret_cast<uint2*>(krow + 32 + d) = make_uint2(pack2(dk1[4 * g] * sc, dk1[4 * g + 1] * sc),
                                                               pack2(dk1[4 * g + 2] * sc, dk1[4 * g + 3] * sc));
-        *reinterpret_cast<uint2*>(vrow + 32 + d) = make_uint2(pack2(dv1[4 * g], dv1[4 * g + 1]),
-                                                              pack2(dv1[4 * g + 2], dv1[4 * g + 3]));
+        *reinterpret_cast<uint2*>(vrow + 32 + d) = make_uint2(pack2(dv1[4 * g] * vs, dv1[4 * g + 1] * vs),
+                                                              pack2(dv1[4 * g + 2] * vs, dv1[4 * g + 3] * vs));
       }
     }
   }
@@ -964,8 +995,10 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
     else attn_bwd_kernel<1><<<grid, 256, BWD_SMEM, stream>>>(a);
   }
   const long n8 = (long)B * T * (H * hd / 8);
+  // dQ = dS K / sqrt(hd); the 256-key kernel multiplied by c K = log2(e) K / sqrt(hd) -> ln 2
+  const float dq_scale = blk256 ? 0.6931471805599453f : 1.f / sqrtf((float)hd);
   attn_dq_finalize_kernel<<<cdiv(n8, 256), 256, 0, stream>>>(dq, dqkv, (long)B * T, H * hd, T,
-                                                             a.dq_part, 1.f / sqrtf((float)hd));
+                                                             a.dq_part, dq_scale);
 }
 
 }  // namespace mg
