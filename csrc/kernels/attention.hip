@@ -65,6 +65,7 @@ struct AttnArgs {
   uint32_t seed_key;   // fwd dropout hash key derived from seed
   uint32_t thr;        // 8-bit keep threshold: keep iff random byte >= thr (0 = no dropout)
   float dscale;        // 1 / (1 - thr/256)
+  uint32_t kadd;       // SWAR keep test: 4 x (128 - thr) if thr <= 128, else 4 x (256 - thr)
 };
 
 MG_DEVICE float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }  // v_exp_f32, no denorm fixup
@@ -185,13 +186,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
       // mask only the tiles that need it (diagonal / past T: wave-uniform), row max on raw scores
       const bool diag = k0 + 63 > q0 + 32 * w;
       if (diag || k0 + 64 > a.T) {
+        // key = k0 + c(sub, r) + 4 h32 with c a constant: one compare against a per-lane limit
+        const int lim = min(myq, a.T - 1) - k0 - 4 * h32;
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = k0 + sub * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
-            if (key > myq || key >= a.T) s[sub][r] = kNegBig;
-          }
+          for (int r = 0; r < 16; ++r)
+            s[sub][r] = (sub * 32 + (r & 3) + 8 * (r >> 2) > lim) ? kNegBig : s[sub][r];
       }
       float mx = s[0][0];
 #pragma unroll
@@ -231,12 +232,20 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
         uint32_t rw[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) rw[i] = mix32(base + (uint32_t)i * 0x9E3779B9u);
+        // SWAR keep test on 4 bytes at once: bit 7 of each byte <- (byte >= thr); the keep word
+        // gets element e = 4i + j (byte j of rw[i]) at bit 8j + i
         uint32_t bits = 0;
 #pragma unroll
-        for (int idx = 31; idx >= 0; --idx) {  // shift-in: element idx ends at bit idx
-          const bool keep = ((rw[idx >> 2] >> (8 * (idx & 3))) & 0xffu) >= a.thr;
-          s[idx >> 4][idx & 15] = keep ? s[idx >> 4][idx & 15] : 0.f;
-          bits = (bits << 1) | (uint32_t)keep;
+        for (int i = 0; i < 8; ++i) {
+          const uint32_t x = rw[i];
+          const uint32_t y = (x & 0x7f7f7f7fu) + a.kadd;
+          const uint32_t k7 = (a.thr <= 128 ? (y | x) : (y & x)) & 0x80808080u;
+          bits |= k7 >> (7 - i);
+        }
+#pragma unroll
+        for (int e = 0; e < 32; ++e) {
+          const int keep = __builtin_amdgcn_sbfe((int)bits, 8 * (e & 3) + (e >> 2), 1);  // 0 / -1
+          s[e >> 4][e & 15] = __int_as_float(__float_as_int(s[e >> 4][e & 15]) & keep);
         }
         if (myq < a.T) a.dmask[(long)drop_row * (2 * ntiles_all) + t * 2 + h32] = bits;
       }
@@ -358,7 +367,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(const AttnArgs a) {
   }
   // this lane's dropout bit inside the forward's keep-words (see attn_fwd_kernel)
   const int mw_col = (w >> 1) * 2 + ((mykey >> 2) & 1);
-  const int mw_bit = ((mykey & 32) >> 1) | (mykey & 3) | (((mykey >> 3) & 3) << 2);
+  const int mw_el = ((mykey & 32) >> 1) | (mykey & 3) | (((mykey >> 3) & 3) << 2);  // fwd element
+  const int mw_bit = 8 * (mw_el & 3) + (mw_el >> 2);  // its bit in the keep word (attn_fwd_kernel)
   const int ntw = 2 * ((a.T + 63) / 64);
   const int t0w = (kb0 / 64) * 2;
 
@@ -645,7 +655,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
   }
   // this lane's dropout bit inside the forward's keep-words (see attn_fwd_kernel)
   const int mw_col = (w >> 1) * 2 + ((mykey >> 2) & 1);
-  const int mw_bit = ((mykey & 32) >> 1) | (mykey & 3) | (((mykey >> 3) & 3) << 2);
+  const int mw_el = ((mykey & 32) >> 1) | (mykey & 3) | (((mykey >> 3) & 3) << 2);  // fwd element
+  const int mw_bit = 8 * (mw_el & 3) + (mw_el >> 2);  // its bit in the keep word (attn_fwd_kernel)
   const int ntw = 2 * ((a.T + 63) / 64);
   const int t0w = (kb0 / 64) * 2;
 
@@ -941,6 +952,7 @@ static AttnArgs make_args(int B, int T, int H, int hd, float p, uint64_t seed) {
   if (p > 0.f) thr = thr < 1 ? 1 : (thr > 255 ? 255 : thr);
   a.thr = (uint32_t)thr;
   a.dscale = thr ? 256.f / (256.f - (float)thr) : 1.f;
+  a.kadd = (uint32_t)(thr <= 128 ? 128 - thr : 256 - thr) * 0x01010101u;
   return a;
 }
 

@@ -105,7 +105,8 @@ def _dense_keep(mask, B, T, H):
     key = torch.arange(T, device=mask.device)
     t, kk = key // 64, key % 64
     col = t * 2 + ((kk >> 2) & 1)
-    bit = ((kk & 32) >> 1) | (kk & 3) | (((kk >> 3) & 3) << 2)
+    el = ((kk & 32) >> 1) | (kk & 3) | (((kk >> 3) & 3) << 2)  # the lane's element index
+    bit = 8 * (el & 3) + (el >> 2)
     w = words[:, col]  # [BHT, T]
     return ((w >> bit) & 1).view(B, H, T, T).float()
 
@@ -135,10 +136,11 @@ def test_attention_dropout_exact(T):
     torch.testing.assert_close(dqkv.float(), g, atol=3e-2 * max(1.0, scale / 4), rtol=5e-2)
 
 
-def test_attention_dropout_keep_rate():
+@pytest.mark.parametrize("p", [0.1, 0.6])  # thr <= 128 and > 128: both SWAR keep tests
+def test_attention_dropout_keep_rate(p):
     """The forward's counter-hash dropout keeps ~(1 - thr/256) of the causal entries, uniformly."""
     C = ext()
-    B, T, H, hd, p = 2, 512, 4, 64, 0.1
+    B, T, H, hd = 2, 512, 4, 64
     qkv = torch.randn(B * T, 3 * H * hd, device=DEV).to(torch.bfloat16)
     _, _, mask = C.attention_fwd(qkv, B, T, H, p, 5)
     keep = _dense_keep(mask, B, T, H)
