@@ -99,6 +99,22 @@ MG_DEVICE bf16x8 lds_tr_frag(const char* base, int r0, int r1, int colbase, int 
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// Byte offset of a transposed-read lane address (row, column) in an lds_off image.
+MG_DEVICE int tr_off(int row, int col) { return lds_off(row, col >> 3) + (col & 7) * 2; }
+
+// Transposed fragment from two precomputed per-lane offsets (rows r0+q and r0+8+q, or +4): the
+// swizzle is periodic in the row with period 16, so a 16-row-aligned row base is a plain byte
+// offset the caller passes as a compile-time constant (it lands in the ds_read offset field)
+// instead of a per-read swizzle computation.
+MG_DEVICE bf16x8 lds_tr_at(const char* base, int oa, int ob) {
+  const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + oa));
+  const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + ob));
+  const s16x8 v = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+MG_DEVICE bf16x8 lds_row_at(const char* base, int o) { return *reinterpret_cast<const bf16x8*>(base + o); }
+
 MG_DEVICE bf16x8 pack_frag(const f32x16& a, int s) {
   s16x8 v;
 #pragma unroll
@@ -694,12 +710,21 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
     const char* sQ = smem + B2_Q;
     const char* sdO = smem + B2_DO;
     int lane = threadIdx.x & 63;
-    asm volatile("" : "+v"(lane));
+    asm volatile("" : "+v"(lane));  // recomputed per tile: keeps the offsets below out of the loop state
     const int h32 = lane >> 5, l32 = lane & 31;
     const bool more = qt + 1 < nqt;
     if (more) issue(qt + 1);
     const int qbase = qt * BQ;
     char* myds = sdS + w * 32 * ROWB;
+    // per-lane LDS offsets for this tile (row bases of 16-row multiples go into immediates):
+    // row reads of row l32, chunk 2 ks + h32; transposed reads rows 4 h32 + q (+8), cols cb + 4p (+32)
+    const char* sKw = sK + w * 32 * ROWB;
+    int ro[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) ro[ks] = lds_off(l32, 2 * ks + h32);
+    const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+    const int ta0 = tr_off(4 * h32 + trq, trc), tb0 = tr_off(8 + 4 * h32 + trq, trc);
+    const int ta1 = tr_off(4 * h32 + trq, 32 + trc), tb1 = tr_off(8 + 4 * h32 + trq, 32 + trc);
 #pragma unroll
     for (int qs = 0; qs < 2; ++qs) {
       const int qsub0 = qbase + qs * 32;
@@ -731,9 +756,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
       for (int r = 0; r < 16; ++r) s[r] = lr[r];  // S' = Q K^T - lse/c
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_frag(sQ, qs * 32 + l32, ks * 2 + h32),
-                                                    lds_row_frag(sK, 32 * w + l32, ks * 2 + h32), s, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_frag(sdO, qs * 32 + l32, ks * 2 + h32), vf[ks], dp, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_at(sQ + qs * 32 * ROWB, ro[ks]),
+                                                    lds_row_at(sKw, ro[ks]), s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_at(sdO + qs * 32 * ROWB, ro[ks]), vf[ks], dp, 0, 0, 0);
       }
       // rows = queries qs*32 + (r&3) + 8(r>>2) + 4*h32 ; col = key (lane).  In place:
       // s <- dropped P (dV operand), dp <- dS = P * (dP~ * Z - delta).
@@ -746,13 +771,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
       for (int st = 0; st < 2; ++st) {
         const bf16x8 pf = pack_frag(s, st);
         const bf16x8 dsf = pack_frag(dp, st);
-        const int r0 = qs * 32 + 16 * st + 4 * h32;
-        const int cb = 16 * ((lane >> 4) & 1);
-        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sdO, r0, r0 + 8, cb, lane), pf, dv0, 0, 0, 0);
-        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sQ, r0, r0 + 8, cb, lane), dsf, dk0, 0, 0, 0);
+        const int rb = (qs * 32 + 16 * st) * ROWB;  // 16-row aligned: an immediate
+        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_at(sdO + rb, ta0, tb0), pf, dv0, 0, 0, 0);
+        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_at(sQ + rb, ta0, tb0), dsf, dk0, 0, 0, 0);
         if constexpr (NKS > 2) {
-          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sdO, r0, r0 + 8, 32 + cb, lane), pf, dv1, 0, 0, 0);
-          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(sQ, r0, r0 + 8, 32 + cb, lane), dsf, dk1, 0, 0, 0);
+          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_at(sdO + rb, ta1, tb1), pf, dv1, 0, 0, 0);
+          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_at(sQ + rb, ta1, tb1), dsf, dk1, 0, 0, 0);
         }
       }
 #pragma unroll
@@ -771,13 +795,15 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
     const bool act0 = dblk * 32 < a.hd && qbase + qs * 32 + 31 >= kb0;
     f32x16 dq = {0};
     if (kh ? act1 : act0) {
-      const int cb = 16 * ((lane >> 4) & 1);
-#pragma unroll 2
-      for (int kk = 0; kk < 8; ++kk) {
-        const int kr0 = kh * 128 + kk * 16 + 8 * h32;
-        const bf16x8 af = lds_tr_frag(sdS, kr0, kr0 + 4, qs * 32 + cb, lane);
-        dq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, lds_tr_frag(sK, kr0, kr0 + 4, dblk * 32 + cb, lane), dq, 0, 0, 0);
-      }
+      // rows kh*128 + 16 kk + 8 h32 + q (+4): the 16 kk part is an immediate
+      const int da = tr_off(8 * h32 + trq, qs * 32 + trc), db = tr_off(8 * h32 + 4 + trq, qs * 32 + trc);
+      const int ka = tr_off(8 * h32 + trq, dblk * 32 + trc), kb = tr_off(8 * h32 + 4 + trq, dblk * 32 + trc);
+      const char* sdSh = sdS + kh * 128 * ROWB;
+      const char* sKh = sK + kh * 128 * ROWB;
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk)
+        dq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_at(sdSh + kk * 16 * ROWB, da, db),
+                                                     lds_tr_at(sKh + kk * 16 * ROWB, ka, kb), dq, 0, 0, 0);
     }
     float* part = reinterpret_cast<float*>(smem + B2_P) + tile * 4 * 64 * 4;
     if (kh == 1 && act1) {
