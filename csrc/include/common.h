@@ -50,6 +50,10 @@ MG_DEVICE uint4 pack8(const float (&f)[8]) {
 }
 
 MG_DEVICE uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
+
+// Opaque to the optimiser: values derived from v before the fence are recomputed after it
+// instead of being kept live (keeps packed bf16 packed across a reduction; see layernorm.hip).
+MG_DEVICE void reg_fence(uint4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
 MG_DEVICE void st16(void* p, const uint4& v) { *reinterpret_cast<uint4*>(p) = v; }
 
 // ---------------------------------------------------------------- wave / block reductions

@@ -87,16 +87,19 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
                                                      float* __restrict__ dw,
                                                      float* __restrict__ db, int M, int D) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  float gacc[NV][8], bacc[NV][8], wf[NV][8];
+  // rows are held PACKED (bf16 x 8 per uint4) between load and use: two rows of x, dy and the
+  // residual gradient in flight cost 3 x 2 x NV x 4 registers instead of twice that as floats
+  // (NV = 4, gpt2-xl's D = 1600, had 504 registers -> one wave per SIMD)
+  float gacc[NV][8], bacc[NV][8];
+  uint4 wraw[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = (i * 64 + lane) * 8;
-    if (c < D) unpack8(ld16(w + c), wf[i]);
+    wraw[i] = c < D ? ld16(w + c) : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       gacc[i][j] = 0.f;
       bacc[i][j] = 0.f;
-      if (c >= D) wf[i][j] = 0.f;
     }
   }
   // two rows per iteration: both rows' loads are issued before either is reduced, so each wave
@@ -104,7 +107,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
   const long stride = (long)gridDim.x * 8;
   for (long r0 = (long)blockIdx.x * 8 + wid; r0 < M; r0 += stride) {
     const long rows[2] = {r0, r0 + 4};
-    float xv[2][NV][8], g[2][NV][8], rv[2][NV][8], mu[2], rs[2];
+    uint4 xr[2][NV], gr[2][NV], rr[2][NV];
+    float mu[2], rs[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const long row = rows[u] < M ? rows[u] : rows[0];
@@ -114,9 +118,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       for (int i = 0; i < NV; ++i) {
         const int c = (i * 64 + lane) * 8;
         if (c < D) {
-          unpack8(ld16(x + row * D + c), xv[u][i]);
-          unpack8(ld16(dy + row * D + c), g[u][i]);
-          if (dres) unpack8(ld16(dres + row * D + c), rv[u][i]);
+          xr[u][i] = ld16(x + row * D + c);
+          gr[u][i] = ld16(dy + row * D + c);
+          if (dres) rr[u][i] = ld16(dres + row * D + c);
         }
       }
     }
@@ -124,22 +128,31 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
     for (int u = 0; u < 2; ++u) {
       if (rows[u] >= M) break;
       const long row = rows[u];
-      float xh[NV][8];
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
         const int c = (i * 64 + lane) * 8;
         if (c < D) {
+          float xv[8], g[8], wf[8];
+          unpack8(xr[u][i], xv);
+          unpack8(gr[u][i], g);
+          unpack8(wraw[i], wf);
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            xh[i][j] = (xv[u][i][j] - mu[u]) * rs[u];
-            const float gw = g[u][i][j] * wf[i][j];
+            const float xh = (xv[j] - mu[u]) * rs[u];
+            const float gw = g[j] * wf[j];
             s1 += gw;
-            s2 += gw * xh[i][j];
-            gacc[i][j] += g[u][i][j] * xh[i][j];
-            bacc[i][j] += g[u][i][j];
+            s2 += gw * xh;
+            gacc[i][j] += g[j] * xh;
+            bacc[i][j] += g[j];
           }
         }
+      }
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        reg_fence(xr[u][i]);
+        reg_fence(gr[u][i]);
+        reg_fence(wraw[i]);
       }
       s1 = wave_sum(s1) / D;
       s2 = wave_sum(s2) / D;
@@ -148,12 +161,18 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       for (int i = 0; i < NV; ++i) {
         const int c = (i * 64 + lane) * 8;
         if (c < D) {
-          float o[8];
+          float xv[8], g[8], wf[8], o[8];
+          unpack8(xr[u][i], xv);
+          unpack8(gr[u][i], g);
+          unpack8(wraw[i], wf);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = rs[u] * (g[u][i][j] * wf[i][j] - s1 - xh[i][j] * s2);
+          for (int j = 0; j < 8; ++j)
+            o[j] = rs[u] * (g[j] * wf[j] - s1 - (xv[j] - mu[u]) * rs[u] * s2);
           if (dres) {  // fused residual-branch gradient: dx = LN'(dy) + dres
+            float rv[8];
+            unpack8(rr[u][i], rv);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) o[j] += rv[u][i][j];
+            for (int j = 0; j < 8; ++j) o[j] += rv[j];
           }
           st16(dxr + c, pack8(o));
         }
