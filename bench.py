@@ -40,8 +40,11 @@ def main():
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--model", default="gpt2")
     ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--vocab", type=int, default=50257, help="65 = chargpt's character vocabulary")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--profile", default="", help="write a torch.profiler trace to this dir")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay each step as one hipGraph (single GPU; StepEngine.graph_step)")
     a = ap.parse_args()
 
     from mingpt_distributed_amd.models import GPT, GPTConfig
@@ -55,7 +58,7 @@ def main():
                   file=sys.stderr)
     N = info.world_size
     torch.manual_seed(1234 + info.rank)
-    cfg = GPTConfig(model_type=a.model, vocab_size=50257, block_size=a.seq, embed_drop=a.dropout,
+    cfg = GPTConfig(model_type=a.model, vocab_size=a.vocab, block_size=a.seq, embed_drop=a.dropout,
                     resid_drop=a.dropout, attn_drop=a.dropout)
     torch.manual_seed(1234)  # identical init on every rank (the engine also broadcasts rank 0)
     model = GPT(cfg, verbose=info.rank == 0)
@@ -63,11 +66,12 @@ def main():
                      bucket_mb=a.bucket_mb)
     g = torch.Generator(device=eng.device).manual_seed(99 + info.rank)
     nb = 4
-    xs = [torch.randint(0, 50257, (a.batch, a.seq), device=eng.device, generator=g) for _ in range(nb)]
-    ys = [torch.randint(0, 50257, (a.batch, a.seq), device=eng.device, generator=g) for _ in range(nb)]
+    xs = [torch.randint(0, a.vocab, (a.batch, a.seq), device=eng.device, generator=g) for _ in range(nb)]
+    ys = [torch.randint(0, a.vocab, (a.batch, a.seq), device=eng.device, generator=g) for _ in range(nb)]
 
+    step = (lambda x, y: eng.graph_step(x, y)) if a.graph else (lambda x, y: eng.train_step([(x, y)]))
     for i in range(a.warmup):
-        loss = eng.train_step([(xs[i % nb], ys[i % nb])])
+        loss = step(xs[i % nb], ys[i % nb])
     D.barrier()
     torch.cuda.synchronize()
     prof = None
@@ -77,7 +81,7 @@ def main():
         prof.__enter__()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        loss = eng.train_step([(xs[i % nb], ys[i % nb])])
+        loss = step(xs[i % nb], ys[i % nb])
     torch.cuda.synchronize()
     D.barrier()
     dt = time.perf_counter() - t0
@@ -94,7 +98,7 @@ def main():
     if info.rank == 0:
         out = {
             "metric": "tokens/sec (whole node), GPT-2 124M seq1024 bf16" if a.model == "gpt2"
-            else f"tokens/sec (whole node), {a.model} seq{a.seq} bf16",
+            else f"tokens/sec (whole node), {a.model} seq{a.seq} vocab{a.vocab} bf16",
             "value": round(value, 1),
             "unit": "tokens/s",
             "n_gpus": N,
@@ -104,12 +108,13 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / (BASELINE_TOK_S_PER_GPU[a.batch] * N), 3)
-            if a.model == "gpt2" and a.seq == 1024 and a.batch in BASELINE_TOK_S_PER_GPU else None,
+            if a.model == "gpt2" and a.seq == 1024 and a.vocab == 50257 and a.batch in BASELINE_TOK_S_PER_GPU
+            else None,
             "dtype": "bf16",
             "data": "synthetic (random tokens, random-init weights)",
             "config": {"model": a.model, "global_batch": a.batch * N, "seq_len": a.seq,
                        "parallelism": f"dp{N}", "micro_batch_per_gpu": a.batch, "dropout": a.dropout,
-                       "bucket_mb": a.bucket_mb},
+                       "bucket_mb": a.bucket_mb, "hip_graph": bool(a.graph and N == 1)},
             "loss": round(loss_v, 4),
             "max_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2),
         }

@@ -65,7 +65,8 @@ at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Te
     CHECK_BF16(*dres); CHECK_CONTIG(*dres);
     TORCH_CHECK(dres->numel() == x.numel(), "layernorm_bwd: dres shape");
   }
-  mg::layernorm_bwd(bp(dy), bp(x), bp(w), fp(mean), fp(rstd), bp_opt(dres), bp(dx), fp(dw), fp(db), nullptr,
+  auto ws = at::empty({(int64_t)mg::layernorm_bwd_workspace((int)M, (int)D)}, mean.options());
+  mg::layernorm_bwd(bp(dy), bp(x), bp(w), fp(mean), fp(rstd), bp_opt(dres), bp(dx), fp(dw), fp(db), fp(ws),
                     (int)M, (int)D, cur_stream());
   return dx;
 }
@@ -124,6 +125,18 @@ at::Tensor xent_bwd(const at::Tensor& logits, const at::Tensor& targets, const a
   mg::xent_bwd(bp(logits), targets.data_ptr<int64_t>(), fp(lse), fp(gscale), fp(out) + 1, bp(dl),
                (int)M, (int)V, (int)ld, cur_stream());
   return dl;
+}
+
+// ------------------------------------------------------------------------------- hipGraph mode
+// While set, launches read dropout-seed offsets from seed_ofs[0] (uint64, bumped inside the graph
+// each replay) and AdamW reads {lr, step} from opt_hp (fp32[2], written before each replay).
+void set_graph_state(const c10::optional<at::Tensor>& seed_ofs, const c10::optional<at::Tensor>& opt_hp) {
+  if (seed_ofs.has_value()) {
+    TORCH_CHECK(seed_ofs->scalar_type() == at::kLong && seed_ofs->is_cuda() && seed_ofs->numel() >= 1);
+  }
+  if (opt_hp.has_value()) { CHECK_F32(*opt_hp); TORCH_CHECK(opt_hp->numel() >= 2); }
+  mg::set_graph_state(seed_ofs.has_value() ? reinterpret_cast<const uint64_t*>(seed_ofs->data_ptr<int64_t>()) : nullptr,
+                      opt_hp.has_value() ? fp(*opt_hp) : nullptr);
 }
 
 // ------------------------------------------------------------------------------- optimizer
@@ -375,6 +388,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embedding_bwd", &embedding_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
+  m.def("set_graph_state", &set_graph_state, py::arg("seed_ofs") = py::none(), py::arg("opt_hp") = py::none());
   m.def("grad_sumsq", &grad_sumsq);
   m.def("adamw_step", &adamw_step);
   m.def("f32_to_bf16", &f32_to_bf16);

@@ -51,6 +51,13 @@ MG_DEVICE uint4 pack8(const float (&f)[8]) {
 
 MG_DEVICE uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
 
+// hipGraph mode: a captured kernel's seed argument is an offset into a per-replay stream whose
+// counter lives in device memory (incremented inside the graph), so every replay draws new
+// dropout masks; nullptr = eager launch, the argument is the seed itself.
+MG_DEVICE uint64_t eff_seed(uint64_t s, const uint64_t* ofs) {
+  return ofs ? s + ofs[0] * 0x9E3779B97F4A7C15ull : s;
+}
+
 // Opaque to the optimiser: values derived from v before the fence are recomputed after it
 // instead of being kept live (keeps packed bf16 packed across a reduction; see layernorm.hip).
 MG_DEVICE void reg_fence(uint4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }

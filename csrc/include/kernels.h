@@ -29,7 +29,10 @@ void xent_fwd(const bf16_t* logits, const int64_t* targets, float* loss_row, flo
 void xent_bwd(const bf16_t* logits, const int64_t* targets, const float* lse, const float* gscale,
               const float* inv_n, bf16_t* dlogits, int M, int V, int ld, hipStream_t stream);
 
-// adamw.hip
+// adamw.hip (also holds the hipGraph-mode device state; see common.h eff_seed)
+void set_graph_state(const uint64_t* seed_ofs, const float* opt_hp);
+const uint64_t* graph_seed_ofs();
+const float* graph_opt_hp();
 size_t grad_norm_workspace();
 void grad_sumsq(const float* grad, long n, float grad_scale, float* workspace, float* out,
                 hipStream_t stream);

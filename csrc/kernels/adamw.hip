@@ -52,7 +52,12 @@ __global__ __launch_bounds__(256) void adamw_kernel(
     const float* __restrict__ chunk_wd, float* __restrict__ master, bf16_t* __restrict__ param,
     const float* __restrict__ grad, float* __restrict__ m, float* __restrict__ v,
     const float* __restrict__ norm, float lr, float b1, float b2, float eps, float bc1,
-    float bc2_sqrt, float grad_scale, float clip) {
+    float bc2_sqrt, float grad_scale, float clip, const float* __restrict__ hp) {
+  if (hp) {  // graph mode: {lr, step} from device memory (the host values were captured once)
+    lr = hp[0];
+    bc1 = 1.f - powf(b1, hp[1]);
+    bc2_sqrt = sqrtf(1.f - powf(b2, hp[1]));
+  }
   const long s0 = chunk_start[blockIdx.x];
   const int len = chunk_len[blockIdx.x];
   const float wd = chunk_wd[blockIdx.x];
@@ -110,6 +115,15 @@ __global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restric
 
 namespace mg {
 
+static const uint64_t* g_seed_ofs = nullptr;
+static const float* g_opt_hp = nullptr;
+void set_graph_state(const uint64_t* seed_ofs, const float* opt_hp) {
+  g_seed_ofs = seed_ofs;
+  g_opt_hp = opt_hp;
+}
+const uint64_t* graph_seed_ofs() { return g_seed_ofs; }
+const float* graph_opt_hp() { return g_opt_hp; }
+
 constexpr int kNormBlocks = 1024;
 
 size_t grad_norm_workspace() { return sizeof(float) * kNormBlocks; }
@@ -128,7 +142,7 @@ void adamw_step(const int64_t* chunk_start, const int* chunk_len, const float* c
   const float bc2_sqrt = sqrtf(1.f - powf(b2, (float)step));
   adamw_kernel<<<n_chunks, 256, 0, stream>>>(chunk_start, chunk_len, chunk_wd, master, param, grad,
                                              m, v, norm, lr, b1, b2, eps, bc1, bc2_sqrt, grad_scale,
-                                             clip);
+                                             clip, g_opt_hp);
 }
 
 void f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t stream) {

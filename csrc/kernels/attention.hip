@@ -63,6 +63,7 @@ struct AttnArgs {
   float scale_log2;    // log2(e) / sqrt(hd)
   uint64_t seed;
   uint32_t seed_key;   // fwd dropout hash key derived from seed
+  const uint64_t* sofs;  // hipGraph mode: seed_key is derived on the device (common.h eff_seed)
   uint32_t thr;        // 8-bit keep threshold: keep iff random byte >= thr (0 = no dropout)
   float dscale;        // 1 / (1 - thr/256)
   uint32_t kadd;       // SWAR keep test: 4 x (128 - thr) if thr <= 128, else 4 x (256 - thr)
@@ -172,6 +173,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
   const int wave_qmax = q0 + 32 * w + 31;
   const uint64_t drop_row = (uint64_t)bh * a.T + myq;
   const int ntiles_all = (a.T + 63) / 64;
+  uint32_t seed_key = a.seed_key;
+  if (a.sofs) {  // same derivation as make_args, from this replay's seed
+    const uint64_t sd = eff_seed(a.seed, a.sofs);
+    seed_key = mix32((uint32_t)sd) ^ mix32((uint32_t)(sd >> 32) + 0x9E3779B9u);
+  }
 
   uint4 rk[2], rv[2];
   load64(rk, Kg, ld, 0, a.T, a.hd);
@@ -244,7 +250,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
         // backward, so this generator never has to be replayed elsewhere); keep iff byte >= thr.
         // The keep scale 1/(1-p) is applied once to O at the end.
         const uint64_t ctr = (drop_row * (uint64_t)ntiles_all + t) * 2 + h32;
-        const uint32_t base = mix32((uint32_t)ctr ^ mix32((uint32_t)(ctr >> 32) ^ a.seed_key));
+        const uint32_t base = mix32((uint32_t)ctr ^ mix32((uint32_t)(ctr >> 32) ^ seed_key));
         uint32_t rw[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) rw[i] = mix32(base + (uint32_t)i * 0x9E3779B9u);
@@ -966,6 +972,7 @@ static AttnArgs make_args(int B, int T, int H, int hd, float p, uint64_t seed) {
   a.B = B; a.T = T; a.H = H; a.hd = hd; a.D = H * hd;
   a.scale_log2 = 1.4426950408889634f / sqrtf((float)hd);
   a.seed = seed;
+  a.sofs = graph_seed_ofs();
   {  // host copy of mix32: per-launch key for the forward's dropout hash
     auto mix = [](uint32_t x) {
       x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;

@@ -43,8 +43,10 @@ __global__ __launch_bounds__(256) void bias_act_kernel(const bf16_t* __restrict_
 
 __global__ __launch_bounds__(256) void bias_drop_resid_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ b, const bf16_t* __restrict__ r,
-    bf16_t* __restrict__ y, long n8, int N, uint64_t seed, uint32_t thr, float scale, int use_drop) {
+    bf16_t* __restrict__ y, long n8, int N, uint64_t seed, uint32_t thr, float scale, int use_drop,
+    const uint64_t* sofs) {
   const uint32_t n8row = (uint32_t)(N >> 3);
+  seed = eff_seed(seed, sofs);
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
     const long e = i * 8;
     const long m = (long)((uint64_t)i / n8row);
@@ -80,8 +82,10 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(const bf16_t* __restrict_
 
 __global__ __launch_bounds__(256) void dropout_bwd_kernel(const bf16_t* __restrict__ dy,
                                                           bf16_t* __restrict__ dx, long n8, int N,
-                                                          uint64_t seed, uint32_t thr, float scale) {
+                                                          uint64_t seed, uint32_t thr, float scale,
+                                                          const uint64_t* sofs) {
   const uint32_t n8row = (uint32_t)(N >> 3);
+  seed = eff_seed(seed, sofs);
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
     const long e = i * 8;
     const long m = (long)((uint64_t)i / n8row);
@@ -98,8 +102,9 @@ __global__ __launch_bounds__(256) void dropout_bias_grad_kernel(const bf16_t* __
                                                                 bf16_t* __restrict__ dx,
                                                                 float* __restrict__ db, int M, int N,
                                                                 uint64_t seed, uint32_t thr,
-                                                                float scale) {
+                                                                float scale, const uint64_t* sofs) {
   __shared__ __attribute__((aligned(16))) float red[4][512];
+  seed = eff_seed(seed, sofs);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 512 + lane * 8;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -221,7 +226,8 @@ void bias_dropout_residual(const bf16_t* x, const bf16_t* b, const bf16_t* r, bf
   const long n8 = M * N / 8;
   const uint32_t thr = dropout_threshold8(p);
   bias_drop_resid_kernel<<<grid_for(n8), 256, 0, stream>>>(x, b, r, y, n8, N, seed, thr,
-                                                           dropout_scale8(thr), thr > 0);
+                                                           dropout_scale8(thr), thr > 0,
+                                                           graph_seed_ofs());
 }
 
 void gelu_bwd(const bf16_t* dy, const bf16_t* pre, bf16_t* dx, long n, hipStream_t stream) {
@@ -232,17 +238,18 @@ void dropout_bwd(const bf16_t* dy, bf16_t* dx, long M, int N, float p, uint64_t 
                  hipStream_t stream) {
   const uint32_t thr = dropout_threshold8(p);
   const long n8 = M * N / 8;
-  dropout_bwd_kernel<<<grid_for(n8), 256, 0, stream>>>(dy, dx, n8, N, seed, thr, dropout_scale8(thr));
+  dropout_bwd_kernel<<<grid_for(n8), 256, 0, stream>>>(dy, dx, n8, N, seed, thr, dropout_scale8(thr),
+                                                       graph_seed_ofs());
 }
 
 void dropout_bias_grad(const bf16_t* dy, bf16_t* dx, float* db, long M, int N, float p, uint64_t seed,
                        hipStream_t stream) {
   const int cx = cdiv(N, 512);
-  int ry = (int)std::min<long>(512, (M + 3) / 4);
+  int ry = (int)std::max<long>(1, std::min<long>(512, M / 64));  // >= 64 rows per block: few atomics
   while (cx * ry > 2048 && ry > 1) ry >>= 1;
   const uint32_t thr = dropout_threshold8(p);
   dropout_bias_grad_kernel<<<dim3(cx, ry), 256, 0, stream>>>(dy, dx, db, (int)M, N, seed, thr,
-                                                             dropout_scale8(thr));
+                                                             dropout_scale8(thr), graph_seed_ofs());
 }
 
 void transpose(const bf16_t* src, bf16_t* dst, int R, int C, int ldd, hipStream_t stream) {
@@ -251,7 +258,7 @@ void transpose(const bf16_t* src, bf16_t* dst, int R, int C, int ldd, hipStream_
 
 void bias_grad(const bf16_t* dy, float* db, long M, int N, hipStream_t stream) {
   const int cx = cdiv(N, 512);
-  int ry = (int)std::min<long>(512, (M + 3) / 4);
+  int ry = (int)std::max<long>(1, std::min<long>(512, M / 64));  // >= 64 rows per block: few atomics
   while (cx * ry > 2048 && ry > 1) ry >>= 1;  // ~2048 blocks: every CU busy, few atomics per column
   bias_grad_kernel<<<dim3(cx, ry), 256, 0, stream>>>(dy, db, (int)M, N);
 }

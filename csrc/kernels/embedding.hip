@@ -20,10 +20,11 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict_
                                                       const bf16_t* __restrict__ wpe,
                                                       bf16_t* __restrict__ out, int M, int T, int D,
                                                       uint64_t seed, uint32_t thr, float scale,
-                                                      int use_dropout) {
+                                                      int use_dropout, const uint64_t* sofs) {
   const int lane = threadIdx.x & 63;
   const long m = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= M) return;
+  seed = eff_seed(seed, sofs);
   const long tok = idx[m];
   const int t = (int)(m % T);
   for (int c = lane * 8; c < D; c += 512) {
@@ -41,10 +42,11 @@ __global__ __launch_bounds__(256) void emb_bwd_wte_kernel(const int64_t* __restr
                                                           const bf16_t* __restrict__ dout,
                                                           float* __restrict__ dwte, int M, int D,
                                                           uint64_t seed, uint32_t thr, float scale,
-                                                          int use_dropout) {
+                                                          int use_dropout, const uint64_t* sofs) {
   const int lane = threadIdx.x & 63;
   const long m = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= M) return;
+  seed = eff_seed(seed, sofs);
   const long tok = idx[m];
   // 8 columns per lane for the load, then 8 atomic instructions each covering 64 x 4 B contiguous.
   for (int c0 = 0; c0 < D; c0 += 512) {
@@ -76,10 +78,11 @@ __global__ __launch_bounds__(256) void emb_bwd_wte_kernel(const int64_t* __restr
 __global__ __launch_bounds__(64) void emb_bwd_wpe_kernel(const bf16_t* __restrict__ dout,
                                                          float* __restrict__ dwpe, int B, int T, int D,
                                                          uint64_t seed, uint32_t thr, float scale,
-                                                         int use_dropout) {
+                                                         int use_dropout, const uint64_t* sofs) {
   const int t = blockIdx.x;
   const int c = blockIdx.y * 512 + threadIdx.x * 8;
   if (c >= D) return;
+  seed = eff_seed(seed, sofs);
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int b = 0; b < B; ++b) {
     const long m = (long)b * T + t;
@@ -102,7 +105,8 @@ void embedding_fwd(const int64_t* idx, const bf16_t* wte, const bf16_t* wpe, bf1
                    int T, int D, float p, uint64_t seed, hipStream_t stream) {
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   emb_fwd_kernel<<<cdiv(M, 4), 256, 0, stream>>>(idx, wte, wpe, out, M, T, D, seed,
-                                                 dropout_threshold(p), scale, p > 0.f);
+                                                 dropout_threshold(p), scale, p > 0.f,
+                                                 graph_seed_ofs());
 }
 
 void embedding_bwd(const int64_t* idx, const bf16_t* dout, float* dwte, float* dwpe, int M, int T,
@@ -111,10 +115,11 @@ void embedding_bwd(const int64_t* idx, const bf16_t* dout, float* dwte, float* d
   const uint32_t thr = dropout_threshold(p);
   if (dwte)
     emb_bwd_wte_kernel<<<cdiv(M, 4), 256, 0, stream>>>(idx, dout, dwte, M, D, seed, thr, scale,
-                                                       p > 0.f);
+                                                       p > 0.f, graph_seed_ofs());
   if (dwpe) {
     dim3 grid(T, cdiv(D, 512));
-    emb_bwd_wpe_kernel<<<grid, 64, 0, stream>>>(dout, dwpe, M / T, T, D, seed, thr, scale, p > 0.f);
+    emb_bwd_wpe_kernel<<<grid, 64, 0, stream>>>(dout, dwpe, M / T, T, D, seed, thr, scale, p > 0.f,
+                                                graph_seed_ofs());
   }
 }
 

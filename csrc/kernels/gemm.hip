@@ -72,6 +72,7 @@ struct GemmArgs {
   bf16_t* aux;     // GELU pre-activation: written (EPI 2) or read (EPI 4); [M, ldc]
   const bf16_t* resid;
   uint64_t seed;
+  const uint64_t* sofs;  // hipGraph mode: per-replay seed counter (common.h eff_seed), else nullptr
   uint32_t thr;
   float scale;
   int tiles_m, tiles_n;
@@ -348,7 +349,7 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
         if constexpr (EPI == 3) {
           if (args.thr) {  // one Philox call per 64-column block of this lane's row (common.h rowdrop)
             const int w16 = (n >> 4) & 3;
-            if (CF::WTN % 64 == 0 ? (j & 3) == 0 : (j == 0 || w16 == 0)) rnd = rowdrop_call(args.seed, m, n, args.N);
+            if (CF::WTN % 64 == 0 ? (j & 3) == 0 : (j == 0 || w16 == 0)) rnd = rowdrop_call(eff_seed(args.seed, args.sofs), m, n, args.N);
             rowdrop4(v, word_of(rnd, CF::WTN % 64 == 0 ? (j & 3) : w16), args.thr, args.scale);
           }
         }
@@ -472,7 +473,7 @@ MG_DEVICE void epilogue(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int 
           if (args.thr) {  // one Philox call per 64-column block of this lane's row (common.h rowdrop)
             // (wave tiles 64 / 128 wide start on a 64-column block; the 96-wide W4 tile may not)
             const int w16 = (n >> 4) & 3;
-            if (CF::WTN % 64 == 0 ? (j & 3) == 0 : (j == 0 || w16 == 0)) rnd = rowdrop_call(args.seed, m, n, args.N);
+            if (CF::WTN % 64 == 0 ? (j & 3) == 0 : (j == 0 || w16 == 0)) rnd = rowdrop_call(eff_seed(args.seed, args.sofs), m, n, args.N);
             rowdrop4(v, word_of(rnd, CF::WTN % 64 == 0 ? (j & 3) : w16), args.thr, args.scale);
           }
           v[0] += bf2f(side[j].x & 0xffffu); v[1] += bf2f(side[j].x >> 16);
@@ -1120,7 +1121,7 @@ void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long l
   a.b_bytes = (uint32_t)std::min<size_t>(b_bytes, 0xFFFFFF00u);
   a.A = A; a.B = B; a.C = C; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.M = M; a.N = N; a.K = K; a.a_ext = a_ext; a.b_ext = b_ext; a.ka = ka; a.kb = kb;
-  a.bias = bias; a.aux = aux; a.resid = resid; a.seed = seed;
+  a.bias = bias; a.aux = aux; a.resid = resid; a.seed = seed; a.sofs = graph_seed_ofs();
   a.thr = dropout_threshold8(p);  // EPI 3 residual dropout: 8-bit row-block mask (common.h)
   a.scale = dropout_scale8(a.thr);
   a.tiles_m = a.tiles_n = a.splits = 1;

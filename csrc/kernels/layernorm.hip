@@ -84,8 +84,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
                                                      const float* __restrict__ rstd,
                                                      const bf16_t* __restrict__ dres,
                                                      bf16_t* __restrict__ dx,
-                                                     float* __restrict__ dw,
-                                                     float* __restrict__ db, int M, int D) {
+                                                     float* __restrict__ part, int M, int D) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   // rows are held PACKED (bf16 x 8 per uint4) between load and use: two rows of x, dy and the
   // residual gradient in flight cost 3 x 2 x NV x 4 registers instead of twice that as floats
@@ -179,9 +178,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       }
     }
   }
-  // fold the 4 waves' column partials through LDS, then one fp32 atomic per column per block
-  // straight into the main-grad buffers (64 contiguous floats per wave-instruction: full-rate
-  // atomic shape; 512 blocks x 2D floats is a few MB of atomic traffic).
+  // fold the 4 waves' column partials through LDS and store the block's partial row
+  // [dgamma | dbeta] with plain stores; ln_colsum_kernel adds the blocks up (a single-stage
+  // atomic fold put every block's atomics on the same 2D addresses)
   extern __shared__ __attribute__((aligned(16))) float red[];  // [4][2*D]
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
@@ -195,8 +194,29 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
     }
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < 2 * D; c += 256) {
-    const float v = red[c] + red[2 * D + c] + red[4 * D + c] + red[6 * D + c];
+  float* prow = part + (long)blockIdx.x * 2 * D;
+  for (int c = threadIdx.x; c < 2 * D; c += 256)
+    prow[c] = red[c] + red[2 * D + c] + red[4 * D + c] + red[6 * D + c];
+}
+
+// dw += sum over blocks of part[:, :D], db += ... part[:, D:].  Block = 64 columns x 4 waves over a
+// 32-row chunk of the G partial rows (8 independent loads per lane: latency, not bandwidth, is
+// what this pass pays); one atomic per column per block (G / 32 per address).
+__global__ __launch_bounds__(256) void ln_colsum_kernel(const float* __restrict__ part, int G, int D,
+                                                        float* __restrict__ dw, float* __restrict__ db) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * 32;
+  float s = 0.f;
+  if (c < 2 * D) {
+    const int r1 = min(G, r0 + 32);
+    for (int r = r0 + wid; r < r1; r += 4) s += part[(long)r * 2 * D + c];
+  }
+  red[wid][lane] = s;
+  __syncthreads();
+  if (wid == 0 && c < 2 * D) {
+    const float v = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
     if (c < D) atomicAdd(dw + c, v);
     else atomicAdd(db + c - D, v);
   }
@@ -206,7 +226,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
 
 namespace mg {
 
-int ln_bwd_grid(int M) { return M / 8 < 1024 ? (M + 7) / 8 : 1024; }  // 2 rows per wave-iteration
+// >= 32 rows per block (4 waves x 2 rows x >= 4 iterations) up to 1024 blocks
+int ln_bwd_grid(int M) { return M / 32 < 1 ? 1 : (M / 32 > 1024 ? 1024 : M / 32); }
 
 #define MG_LN_DISPATCH(KERNEL, ...)                                                   \
   do {                                                                                \
@@ -228,9 +249,11 @@ void layernorm_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const flo
                    float* workspace, int M, int D, hipStream_t stream) {
   const int grid = ln_bwd_grid(M);
   const size_t smem = sizeof(float) * 8 * D;
-  MG_LN_DISPATCH(ln_bwd_kernel, dy, x, w, mean, rstd, dres, dx, dw, db, M, D);
+  MG_LN_DISPATCH(ln_bwd_kernel, dy, x, w, mean, rstd, dres, dx, workspace, M, D);
+  ln_colsum_kernel<<<dim3(cdiv(2 * D, 64), cdiv(grid, 32)), 256, 0, stream>>>(workspace, grid, D, dw, db);
 }
 
-size_t layernorm_bwd_workspace(int M, int D) { return 0; }
+// floats of partial [dgamma | dbeta] rows layernorm_bwd needs
+size_t layernorm_bwd_workspace(int M, int D) { return (size_t)ln_bwd_grid(M) * 2 * D; }
 
 }  // namespace mg

@@ -131,6 +131,65 @@ class StepEngine:
         self.optimizer_step()
         return total / n
 
+    # ------------------------------------------------------------------ hipGraph step
+    def graph_step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        """``train_step([(x, y)])`` as ONE hipGraph replay (single process, GPU).
+
+        The whole step -- embedding, every block's fused kernels, head + loss, backward, grad-norm,
+        AdamW, grad zeroing -- is captured once per input shape and replayed: one launch per step
+        instead of ~20 per layer from Python, which is what bounds small models (chargpt's
+        gpt-mini at T=128 is launch-bound) and removes host jitter for large ones.  What changes
+        per step lives in device memory: the inputs (copied into static buffers), a dropout seed
+        counter bumped inside the graph (common.h eff_seed: every replay draws new masks), and
+        AdamW's {lr, step} written before each replay.  Returns the step's loss (a static buffer,
+        overwritten by the next replay)."""
+        if self.device.type != "cuda" or self.dp is not None:
+            return self.train_step([(x, y)])
+        from .ops._ext import ext
+
+        C = ext()
+        key = (tuple(x.shape), tuple(y.shape))
+        g = getattr(self, "_graph", None)
+        if g is None or g["key"] != key:
+            g = self._capture(C, key, x, y)
+        g["x"].copy_(x, non_blocking=True)
+        g["y"].copy_(y, non_blocking=True)
+        self.opt.step_count += 1
+        g["hp"][0].fill_(float(self.opt.param_groups[0]["lr"]))
+        g["hp"][1].fill_(float(self.opt.step_count))
+        g["graph"].replay()
+        return g["loss"]
+
+    def _capture(self, C, key, x, y):
+        self._graph = None
+        dev = self.device
+        st = {"key": key, "x": torch.empty_like(x, device=dev), "y": torch.empty_like(y, device=dev),
+              "hp": torch.zeros(2, dtype=torch.float32, device=dev),
+              "seed": torch.zeros(1, dtype=torch.int64, device=dev)}
+        st["x"].copy_(x)
+        st["y"].copy_(y)
+        # warm up on a side stream (allocator / autograd state), as torch.cuda.graph requires;
+        # these are real optimizer steps, so they count
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                self.train_step([(st["x"], st["y"])])
+        torch.cuda.current_stream(dev).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        C.set_graph_state(st["seed"], st["hp"])
+        n0 = self.opt.step_count
+        try:
+            with torch.cuda.graph(graph):
+                st["seed"].add_(1)
+                st["loss"] = self.train_step([(st["x"], st["y"])])
+        finally:
+            C.set_graph_state(None, None)
+            self.opt.step_count = n0  # the captured step ran no update; replays advance it
+        st["graph"] = graph
+        self._graph = st
+        return st
+
     @property
     def grad_norm(self) -> torch.Tensor:
         return self.opt.grad_norm
@@ -466,6 +525,7 @@ class Trainer:
         C.weight_decay = 0.1
         C.grad_norm_clip = 1.0
         C.grad_accum_steps = 1
+        C.cuda_graph = False  # replay each step as one hipGraph (StepEngine.graph_step; 1 GPU)
         return C
 
     def __init__(self, config, model, train_dataset):
@@ -513,9 +573,13 @@ class Trainer:
         self.iter_time = time.time()
         data_iter = iter(loader)
         accum = max(1, getattr(config, "grad_accum_steps", 1))
+        graph = bool(getattr(config, "cuda_graph", False)) and accum == 1
         while True:
             batches = [next(data_iter) for _ in range(accum)]
-            self.loss = self.engine.train_step(batches)
+            if graph:
+                self.loss = self.engine.graph_step(*batches[0])
+            else:
+                self.loss = self.engine.train_step(batches)
             self.trigger_callbacks("on_batch_end")
             self.iter_num += 1
             tnow = time.time()

@@ -34,6 +34,7 @@ def get_config():
     C.trainer.learning_rate = 5e-4
     C.trainer.max_iters = 2000
     C.trainer.num_workers = 0
+    C.trainer.cuda_graph = True  # gpt-mini at T=128 is launch-bound: one hipGraph replay per step
     C.sample_every = 500
     return C
 
