@@ -22,6 +22,17 @@ from ._ext import ext
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_RESID, EPI_GELU_BWD = 0, 1, 2, 3, 4
 
 
+_MAX_BYTES = 0xFFFFFF00  # the kernels address each operand through a 32-bit buffer descriptor
+
+
+def _row_chunks(M: int, *row_bytes: int):
+    """Row ranges [r0, r1) of an M-row operand such that no chunk of any operand whose rows are
+    ``row_bytes`` wide reaches 4 GiB (e.g. GPT-2 logits at > 42k tokens per GPU): the M-chunked
+    launches are exact (the epilogues used here do not depend on the global row index)."""
+    step = max(256, (_MAX_BYTES // max(max(row_bytes), 1)) // 256 * 256)
+    return [(r0, min(M, r0 + step)) for r0 in range(0, M, step)]
+
+
 def _check2d(t, name):
     if t.dim() != 2 or not t.is_contiguous():
         raise ValueError(f"{name} must be a contiguous 2-D tensor, got {tuple(t.shape)}")
@@ -44,8 +55,14 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: Optional[torch.Tensor] = 
             "gelu_bwd": EPI_GELU_BWD}[epi]
     if code == EPI_BIAS and bias is None:
         code = EPI_NONE
-    ext().gemm(a, b, c, 0, code, bias, aux if code == EPI_GELU_BWD else pre_out, resid, float(p),
-               int(seed), M, N, dbias)
+    side = aux if code == EPI_GELU_BWD else pre_out
+    chunks = _row_chunks(M, 2 * K, 2 * ld)
+    if len(chunks) > 1 and code == EPI_RESID and p > 0:
+        raise ValueError("gemm_nt: residual dropout keys its mask on the global row; operand too large")
+    for r0, r1 in chunks:
+        sl = (lambda t: t if t is None or len(chunks) == 1 else t[r0:r1])
+        ext().gemm(sl(a), b, sl(c), 0, code, bias, sl(side), sl(resid), float(p), int(seed), r1 - r0, N,
+                   dbias)
     return c
 
 
@@ -74,7 +91,10 @@ def gemm_nn(a: torch.Tensor, b: torch.Tensor, *, epi: str = "none",
     N = b.shape[1]
     c = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
     code = {"none": EPI_NONE, "gelu_bwd": EPI_GELU_BWD}[epi]
-    ext().gemm(a, b, c, 1, code, None, aux, None, 0.0, 0, M, N)
+    chunks = _row_chunks(M, 2 * K, 2 * N)
+    for r0, r1 in chunks:
+        sl = (lambda t: t if t is None or len(chunks) == 1 else t[r0:r1])
+        ext().gemm(sl(a), b, sl(c), 1, code, None, sl(aux), None, 0.0, 0, r1 - r0, N)
     return c
 
 
@@ -88,5 +108,7 @@ def gemm_tn_acc(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, n_valid: Opti
         N = n_valid
     if c.dtype != torch.float32 or c.shape[0] < N or c.shape[1] != K:
         raise ValueError("gemm_tn_acc: c must be fp32 [N, K]")
-    ext().gemm(a, b, c, 2, EPI_NONE, None, None, None, 0.0, 0, N, K)
+    # the reduction runs over M: chunks accumulate into c one after another
+    for r0, r1 in _row_chunks(M, 2 * a.shape[1], 2 * K):
+        ext().gemm(a[r0:r1], b[r0:r1], c, 2, EPI_NONE, None, None, None, 0.0, 0, N, K)
     return c

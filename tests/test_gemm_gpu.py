@@ -128,3 +128,29 @@ def test_dgrad_gelu_bwd_bias_grad():
     db = torch.ones(Nin, device=DEV)
     out = G.gemm_dgrad(dy, w, epi="gelu_bwd", aux=gd.contiguous(), dbias=db)
     torch.testing.assert_close(db, 1 + out.float().sum(0), atol=5e-1, rtol=1e-2)
+
+
+def test_row_chunked_launches_match(monkeypatch):
+    """Operands past 4 GiB (GPT-2 logits beyond ~42k tokens per GPU) are launched in M-chunks:
+    force tiny chunks and compare against single launches."""
+    from mingpt_distributed_amd.ops import gemm as G
+
+    torch.manual_seed(0)
+    M, K, N = 1000, 192, 320
+    r = lambda *s: (torch.randn(*s, device="cuda") * 0.5).to(torch.bfloat16)
+    a, w, bias = r(M, K), r(N, K), r(N)
+    dy = r(M, N)
+    ref_nt = G.gemm_nt(a, w, bias=bias, epi="bias")
+    pre_ref = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    ref_gelu = G.gemm_nt(a, w, bias=bias, epi="gelu", pre_out=pre_ref)
+    ref_nn = G.gemm_nn(dy, w)
+    ref_tn = G.gemm_tn_acc(dy, a, torch.zeros(N, K, device="cuda"))
+    monkeypatch.setattr(G, "_MAX_BYTES", 256 * 2 * max(K, N))  # 256-row chunks
+    assert len(G._row_chunks(M, 2 * K, 2 * N)) == 4
+    torch.testing.assert_close(G.gemm_nt(a, w, bias=bias, epi="bias"), ref_nt, atol=0, rtol=0)
+    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    torch.testing.assert_close(G.gemm_nt(a, w, bias=bias, epi="gelu", pre_out=pre), ref_gelu, atol=0, rtol=0)
+    torch.testing.assert_close(pre, pre_ref, atol=0, rtol=0)
+    torch.testing.assert_close(G.gemm_nn(dy, w), ref_nn, atol=0, rtol=0)
+    torch.testing.assert_close(G.gemm_tn_acc(dy, a, torch.zeros(N, K, device="cuda")), ref_tn,
+                               atol=1e-3, rtol=1e-4)
