@@ -29,7 +29,9 @@ def _row_chunks(M: int, *row_bytes: int):
     """Row ranges [r0, r1) of an M-row operand such that no chunk of any operand whose rows are
     ``row_bytes`` wide reaches 4 GiB (e.g. GPT-2 logits at > 42k tokens per GPU): the M-chunked
     launches are exact (the epilogues used here do not depend on the global row index)."""
-    step = max(256, (_MAX_BYTES // max(max(row_bytes), 1)) // 256 * 256)
+    cap = max(256, (_MAX_BYTES // max(max(row_bytes), 1)) // 256 * 256)
+    n = -(-M // cap)
+    step = min(cap, -(-(-(-M // n)) // 256) * 256)  # balanced: equal tile counts per launch
     return [(r0, min(M, r0 + step)) for r0 in range(0, M, step)]
 
 
