@@ -13,6 +13,8 @@ fixed), embedding ``model.py:193-231``, head + loss ``model.py:309-320``.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import gemm as G
@@ -117,6 +119,24 @@ class TransformerBlockFn(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------------------------ head + loss
+# The LM head's forward and data-gradient GEMMs carry no epilogue (plain [M, 768] x [768, 50304]
+# and [M, 50304] x [50304, 768]): they go to the library GEMM (hipBLASLt via torch.mm), which beat
+# the hand-written W4 kernel on exactly these two shapes by 2.3 ms per B=64 step (one-box A/B,
+# PERF.md).  The weight gradient (fp32 accumulate into main_grad) and every fused GEMM stay on the
+# HIP kernels.  MINGPT_LMHEAD_BLAS=0 routes the head through gemm.hip as well.
+_LMHEAD_BLAS = os.environ.get("MINGPT_LMHEAD_BLAS", "1") == "1"
+
+
+def _padded_weight(w, ld):
+    """[ld, D] copy of W with zero rows past V (cached per weight; refreshed every call)."""
+    wp = getattr(w, "_mg_padded", None)
+    if wp is None or wp.shape[0] != ld:
+        wp = torch.zeros(ld, w.shape[1], dtype=w.dtype, device=w.device)
+        w._mg_padded = wp
+    wp[: w.shape[0]].copy_(w)
+    return wp
+
+
 class HeadLossFn(torch.autograd.Function):
     """loss = CE(LN_f(x) @ W^T, targets) with padded-vocab logits; returns (logits[M, Vpad], loss)."""
 
@@ -126,7 +146,12 @@ class HeadLossFn(torch.autograd.Function):
         V = w.shape[0]
         ld = (V + 127) // 128 * 128
         h, mean, rstd = C.layernorm_fwd(x, lnw, lnb, eps)
-        logits = G.gemm_nt(h, w, ld=ld)
+        ctx.wpad = None
+        if _LMHEAD_BLAS:
+            ctx.wpad = _padded_weight(w, ld)
+            logits = torch.mm(h, ctx.wpad.t())
+        else:
+            logits = G.gemm_nt(h, w, ld=ld)
         out, lse = C.xent_fwd(logits, targets, V)
         ctx.save_for_backward(x, h, mean, rstd, logits, targets, lse, out)
         ctx.params = (lnw, lnb, w)
@@ -148,7 +173,10 @@ class HeadLossFn(torch.autograd.Function):
         del logits
         bw, mw = grad_target(w)
         G.gemm_tn_acc(dlogits, h, bw, n_valid=V)
-        dh = G.gemm_dgrad(dlogits, w)  # W^T padded to the logits' row stride (zero columns)
+        if ctx.wpad is not None:
+            dh = torch.mm(dlogits, ctx.wpad)  # zero rows past V meet the zero pad columns
+        else:
+            dh = G.gemm_dgrad(dlogits, w)  # W^T padded to the logits' row stride (zero columns)
         blw, mlw = grad_target(lnw)
         blb, mlb = grad_target(lnb)
         dx = C.layernorm_bwd(dh, x, lnw, mean, rstd, blw, blb, None)
