@@ -76,12 +76,14 @@ class GPT(nn.Module):
             if prm.dim() >= 2:
                 nn.init.normal_(prm, 0.0, 0.02 / math.sqrt(2 * L) if n.endswith("c_proj.weight") else 0.02)
 
-    def forward(self, idx, targets):
+    def forward(self, idx, targets=None):
         T = idx.size(1)
         x = self.drop(self.wte(idx) + self.wpe(torch.arange(T, device=idx.device)))
         for b in self.h:
             x = b(x)
         logits = self.lm_head(self.ln_f(x))
+        if targets is None:
+            return logits, None
         return logits, F.cross_entropy(logits.view(-1, logits.size(-1)), targets.view(-1), ignore_index=-1)
 
 
@@ -94,8 +96,10 @@ def main():
     ap.add_argument("--attn", default="math", choices=["math", "sdpa"])
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--model", default="gpt2")
+    ap.add_argument("--vocab", type=int, default=50257)
     a = ap.parse_args()
-    dims = {"gpt2": (12, 12, 768), "gpt2-xl": (48, 25, 1600), "gpt2-medium": (24, 16, 1024)}[a.model]
+    dims = {"gpt2": (12, 12, 768), "gpt2-xl": (48, 25, 1600), "gpt2-medium": (24, 16, 1024),
+            "gpt-mini": (6, 6, 192)}[a.model]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -103,12 +107,12 @@ def main():
     if world > 1:
         torch.distributed.init_process_group("nccl")
     torch.manual_seed(0)
-    model = GPT(T=a.seq, L=dims[0], H=dims[1], D=dims[2], p=a.dropout, attn=a.attn).cuda()
+    model = GPT(V=a.vocab, T=a.seq, L=dims[0], H=dims[1], D=dims[2], p=a.dropout, attn=a.attn).cuda()
     if world > 1:
         model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local])
     opt = torch.optim.AdamW(model.parameters(), lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1)
-    x = torch.randint(0, 50257, (a.batch, a.seq), device="cuda")
-    y = torch.randint(0, 50257, (a.batch, a.seq), device="cuda")
+    x = torch.randint(0, a.vocab, (a.batch, a.seq), device="cuda")
+    y = torch.randint(0, a.vocab, (a.batch, a.seq), device="cuda")
 
     def step():
         with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -139,7 +143,7 @@ def main():
     if rank == 0:
         print(json.dumps({"metric": "baseline_torch_eager_tokens_per_s", "value": tok, "n_gpus": world,
                           "ms_per_step": dt / a.steps * 1e3, "batch_per_gpu": a.batch, "seq": a.seq,
-                          "attn": a.attn, "dropout": a.dropout, "model": a.model,
+                          "attn": a.attn, "dropout": a.dropout, "model": a.model, "vocab": a.vocab,
                           "loss": float(loss.item()),
                           "max_mem_gb": torch.cuda.max_memory_allocated() / 2**30}), flush=True)
     if world > 1:

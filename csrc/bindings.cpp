@@ -364,8 +364,30 @@ at::Tensor attention_bwd(const at::Tensor& qkv, const at::Tensor& out, const at:
   return dqkv;
 }
 
+// y[B, ldy] (ldy >= N) = epi(x[B, K] @ W[N, K]^T): the decode-time projection (gemv.hip)
+at::Tensor gemv(const at::Tensor& x, const at::Tensor& W, int64_t epi, const c10::optional<at::Tensor>& bias,
+                const c10::optional<at::Tensor>& resid, int64_t ldy) {
+  CHECK_BF16(x); CHECK_BF16(W); CHECK_CONTIG(x); CHECK_CONTIG(W);
+  const int64_t K = W.size(1), N = W.size(0), B = x.numel() / K;
+  TORCH_CHECK(x.size(-1) == K && mg::gemv_supported((int)B, (int)K), "gemv: B <= 8, K % 8 == 0, K <= 4096");
+  if (ldy <= 0) ldy = N;
+  TORCH_CHECK(ldy >= N && epi >= 0 && epi <= 3, "gemv: ldy / epi");
+  if (bias.has_value()) { CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == N); }
+  if (epi == 3) {
+    TORCH_CHECK(resid.has_value(), "gemv: residual epilogue needs resid");
+    CHECK_BF16(*resid); CHECK_CONTIG(*resid);
+    TORCH_CHECK(resid->numel() == B * ldy, "gemv: resid shape");
+  }
+  DevGuard g(x.device());
+  auto y = at::empty({B, ldy}, x.options());
+  mg::gemv(bp(x), bp(W), bp(y), (int)B, (int)N, (int)K, ldy, bias.has_value() ? bp(*bias) : nullptr,
+           epi == 3 ? bp(*resid) : nullptr, (int)epi, cur_stream());
+  return y;
+}
+
+// pos_dev (int32 [1] on the device, optional): the position is read by the kernel (hipGraph decode)
 at::Tensor attention_decode(const at::Tensor& qkv_new, const at::Tensor& cache, int64_t H,
-                            int64_t pos) {
+                            int64_t pos, const c10::optional<at::Tensor>& pos_dev) {
   CHECK_BF16(qkv_new); CHECK_BF16(cache); CHECK_CONTIG(qkv_new); CHECK_CONTIG(cache);
   TORCH_CHECK(cache.dim() == 3, "cache must be [B, Tmax, 3D]");
   const int64_t B = cache.size(0), Tmax = cache.size(1), D3 = cache.size(2), D = D3 / 3;
@@ -373,8 +395,13 @@ at::Tensor attention_decode(const at::Tensor& qkv_new, const at::Tensor& cache, 
   TORCH_CHECK(pos >= 0 && pos < Tmax && (D / H) % 8 == 0, "attention_decode: pos / head dim");
   DevGuard g(cache.device());
   auto out = at::empty({B, D}, cache.options());
+  const int* pd = nullptr;
+  if (pos_dev.has_value()) {
+    TORCH_CHECK(pos_dev->scalar_type() == at::kInt && pos_dev->is_cuda(), "pos_dev must be int32 cuda");
+    pd = pos_dev->data_ptr<int>();
+  }
   mg::attention_decode(bp(qkv_new), bp(cache), bp(out), (int)B, (int)H, (int)(D / H), Tmax, (int)pos,
-                       cur_stream());
+                       cur_stream(), pd);
   return out;
 }
 
@@ -407,5 +434,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_get_variant", &mg::gemm_get_variant);
   m.def("attention_fwd", &attention_fwd);
   m.def("attention_bwd", &attention_bwd);
-  m.def("attention_decode", &attention_decode);
+  m.def("gemv", &gemv, py::arg("x"), py::arg("W"), py::arg("epi"), py::arg("bias") = py::none(),
+        py::arg("resid") = py::none(), py::arg("ldy") = 0);
+  m.def("gemv_supported", &mg::gemv_supported);
+  m.def("attention_decode", &attention_decode, py::arg("qkv_new"), py::arg("cache"), py::arg("H"),
+        py::arg("pos"), py::arg("pos_dev") = py::none());
 }

@@ -42,6 +42,11 @@ void adamw_step(const int64_t* chunk_start, const int* chunk_len, const float* c
                 float grad_scale, float clip, hipStream_t stream);
 void f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t stream);
 
+// gemv.hip (decode-time skinny GEMM, B <= 8 rows; epi 0 none, 1 bias, 2 bias+GELU, 3 bias+residual)
+bool gemv_supported(int B, int K);
+void gemv(const bf16_t* x, const bf16_t* W, bf16_t* y, int B, int N, int K, long ldy, const bf16_t* bias,
+          const bf16_t* resid, int epi, hipStream_t stream);
+
 // elementwise.hip
 void bias_act_fwd(const bf16_t* x, const bf16_t* b, bf16_t* pre, bf16_t* y, long M, int N, int act,
                   hipStream_t stream);
@@ -80,6 +85,7 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
 
 // one decode step: appends K/V of qkv_new [B, 3D] at row pos of cache [B, Tmax, 3D]; out [B, D]
 void attention_decode(const bf16_t* qkv_new, bf16_t* cache, bf16_t* out, int B, int H, int hd,
-                      long Tmax, int pos, hipStream_t stream);
+                      long Tmax, int pos, hipStream_t stream,
+                      const int* pos_dev = nullptr);
 
 }  // namespace mg

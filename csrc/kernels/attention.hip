@@ -898,7 +898,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
                                                           bf16_t* __restrict__ cache,
                                                           bf16_t* __restrict__ out, int H, int hd,
                                                           int D, long Tmax, int pos,
+                                                          const int* __restrict__ pos_dev,
                                                           float scale_log2) {
+  if (pos_dev) pos = min(max(*pos_dev, 0), (int)Tmax - 1);  // hipGraph decode: position in device memory
   extern __shared__ __attribute__((aligned(16))) float dsm[];  // [64 q][Tmax scores][4*64 acc][8]
   float* qs = dsm;
   float* sc = dsm + 64;
@@ -959,10 +961,10 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
 namespace mg {
 
 void attention_decode(const bf16_t* qkv_new, bf16_t* cache, bf16_t* out, int B, int H, int hd,
-                      long Tmax, int pos, hipStream_t stream) {
+                      long Tmax, int pos, hipStream_t stream, const int* pos_dev) {
   const size_t smem = sizeof(float) * (64 + ((Tmax + 3) & ~3L) + 4 * 64 + 8);
   attn_decode_kernel<<<B * H, 256, smem, stream>>>(qkv_new, cache, out, H, hd, H * hd, Tmax, pos,
-                                                   1.4426950408889634f / sqrtf((float)hd));
+                                                   pos_dev, 1.4426950408889634f / sqrtf((float)hd));
 }
 
 static int g_attn_bwd_variant = 0;  // 0 auto (256-key blocks), 1 force 128-key blocks

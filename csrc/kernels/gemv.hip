@@ -1,0 +1,110 @@
+// Skinny GEMM ("GEMV") for autoregressive decode on gfx950.
+//
+// One decode step pushes B <= 8 rows through every projection of the model
+// (/root/reference/mingpt/model.py:322-356 re-runs the whole prefix instead; the KV-cache path in
+// models/generation.py needs only the new token's rows).  At M = B the MFMA GEMM has 1 row tile:
+// 6-24 workgroups walk a K loop one tile at a time and the projection is latency-bound
+// (26 us for the 3072 -> 768 MLP projection at B = 1).  The work is a stream of the weight
+// matrix (K x N bf16, read once) against B vectors that fit in LDS, so here:
+//   * x [B, K] is staged once per workgroup in LDS;
+//   * a wave owns 4 output columns n: lanes 16g..16g+15 read row n = W[n, :] in 16-byte chunks
+//     (4 x 256 B contiguous segments per wave-instruction, 4 loads in flight per lane), FMA
+//     against the B vectors from LDS;
+//   * the 16 lanes of a row group fold with 4 xor-shuffles; lane 16g writes y[b, n] with the same
+//     fused epilogues as gemm.hip's forward (bias | bias + GELU | residual + bias), no dropout
+//     (inference).
+#include "common.h"
+#include "kernels.h"
+
+using namespace mg;
+
+namespace {
+
+constexpr int kGemvMaxB = 8;
+constexpr int kGemvMaxK = 4096;  // B x K bf16 of x must fit the LDS staging buffer
+
+template <int B>
+__global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ x,
+                                                   const bf16_t* __restrict__ W,
+                                                   bf16_t* __restrict__ y, int N, int K, long ldy,
+                                                   const bf16_t* __restrict__ bias,
+                                                   const bf16_t* __restrict__ resid, int epi) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t xs[];  // [B][K]
+  for (int i = threadIdx.x * 8; i < B * K; i += 256 * 8) st16(xs + i, ld16(x + i));
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int g = lane >> 4, j = lane & 15;  // 4 rows per wave, 16 lanes (256 B) per row segment
+  const int n = (blockIdx.x * 4 + wid) * 4 + g;
+  float acc[B];
+#pragma unroll
+  for (int b = 0; b < B; ++b) acc[b] = 0.f;
+  if (n < N) {
+    const bf16_t* wr = W + (long)n * K;
+    int c = j * 8;
+    for (; c + 3 * 128 < K; c += 4 * 128) {  // 4 loads in flight per lane
+      uint4 wv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) wv[u] = ld16(wr + c + u * 128);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float wf[8];
+        unpack8(wv[u], wf);
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+          float xf[8];
+          unpack8(ld16(xs + b * K + c + u * 128), xf);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[b] = __builtin_fmaf(wf[e], xf[e], acc[b]);
+        }
+      }
+    }
+    for (; c < K; c += 128) {
+      float wf[8];
+      unpack8(ld16(wr + c), wf);
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        float xf[8];
+        unpack8(ld16(xs + b * K + c), xf);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[b] = __builtin_fmaf(wf[e], xf[e], acc[b]);
+      }
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) acc[b] += __shfl_xor(acc[b], o, 64);
+  }
+  if (n < N && j == 0) {
+    const float bv = bias ? bf2f(bias[n]) : 0.f;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      float v = acc[b] + bv;
+      if (epi == 2) v = gelu_f(v);
+      if (epi == 3) v += bf2f(resid[(long)b * ldy + n]);
+      y[(long)b * ldy + n] = f2bf(v);
+    }
+  }
+}
+
+}  // namespace
+
+namespace mg {
+
+bool gemv_supported(int B, int K) { return B >= 1 && B <= kGemvMaxB && K % 8 == 0 && K <= kGemvMaxK; }
+
+void gemv(const bf16_t* x, const bf16_t* W, bf16_t* y, int B, int N, int K, long ldy, const bf16_t* bias,
+          const bf16_t* resid, int epi, hipStream_t stream) {
+  const int grid = cdiv(N, 16);  // 4 waves x 4 rows
+  const size_t smem = sizeof(bf16_t) * (size_t)B * K;
+#define MG_GEMV_CASE(b) \
+  case b: gemv_kernel<b><<<grid, 256, smem, stream>>>(x, W, y, N, K, ldy, bias, resid, epi); break;
+  switch (B) {  // exact row counts: the kernel stages and writes exactly B rows
+    MG_GEMV_CASE(1) MG_GEMV_CASE(2) MG_GEMV_CASE(3) MG_GEMV_CASE(4)
+    MG_GEMV_CASE(5) MG_GEMV_CASE(6) MG_GEMV_CASE(7) MG_GEMV_CASE(8)
+    default: break;
+  }
+#undef MG_GEMV_CASE
+}
+
+}  // namespace mg

@@ -23,6 +23,8 @@ from ..ops import reference as R
 
 
 def _sample(logits, temperature, do_sample, top_k):
+    if not do_sample:  # greedy: top-1 of softmax(logits / t) is the argmax of the logits
+        return logits.argmax(dim=-1, keepdim=True)
     logits = logits.float() / temperature
     if top_k is not None:
         v, _ = torch.topk(logits, min(top_k, logits.size(-1)))
@@ -99,7 +101,9 @@ class _GpuCache:
                        for _ in range(cfg.n_layer)]
         self.logits = self._run(idx, 0)
 
-    def _run(self, idx, pos0):
+    def _run(self, idx, pos0, pos_dev=None):
+        """Prefill (pos0 == 0) or one decode step at position pos0 (or at ``pos_dev[0]``, an int32
+        device scalar, when captured in a hipGraph)."""
         C, G, bf = self.C, self.G, self.bf
         m = self.model
         tr, cfg = m.transformer, m.config
@@ -109,30 +113,63 @@ class _GpuCache:
         if pos0 == 0:
             x = C.embedding_fwd(idx.contiguous(), bf(tr.wte.weight), wpe, 0.0, 0).view(B * T, D)
         else:  # single token at position pos0
-            x = C.embedding_fwd(idx.contiguous(), bf(tr.wte.weight), wpe[pos0:pos0 + 1].contiguous(),
-                                0.0, 0).view(B * T, D)
+            wrow = wpe.index_select(0, pos_dev) if pos_dev is not None else wpe[pos0:pos0 + 1].contiguous()
+            x = C.embedding_fwd(idx.contiguous(), bf(tr.wte.weight), wrow, 0.0, 0).view(B * T, D)
+        # decode rows (B <= 8) go through the skinny GEMM (gemv.hip): at M = B the MFMA GEMM has
+        # one row tile and walks K latency-bound; prefill uses the MFMA GEMM
+        skinny = pos0 > 0 and C.gemv_supported(B * T, 4 * D)
+
+        def lin(inp, w, b, epi, resid=None, ld=0):
+            if skinny:
+                code = {"none": 0, "bias": 1, "gelu": 2, "resid": 3}[epi]
+                return C.gemv(inp, bf(w), code, bf(b) if b is not None else None, resid, ld)
+            if epi == "gelu":
+                pre = torch.empty((inp.shape[0], w.shape[0]), dtype=torch.bfloat16, device=inp.device)
+                return G.gemm_nt(inp, bf(w), bias=bf(b), epi="gelu", pre_out=pre)
+            return G.gemm_nt(inp, bf(w), bias=bf(b) if b is not None else None, epi=epi, resid=resid,
+                             ld=ld or None)
+
         for i, blk in enumerate(tr.h):
             a, mm = blk.attn, blk.mlp
             h, _, _ = C.layernorm_fwd(x, bf(blk.ln_1.weight), bf(blk.ln_1.bias), eps)
-            qkv = G.gemm_nt(h, bf(a.c_attn.weight), bias=bf(a.c_attn.bias), epi="bias")
+            qkv = lin(h, a.c_attn.weight, a.c_attn.bias, "bias")
             if pos0 == 0:
                 self.caches[i][:, :T].copy_(qkv.view(B, T, 3 * D))
                 y, _, _ = C.attention_fwd(qkv, B, T, H, 0.0, 0)
             else:
-                y = C.attention_decode(qkv, self.caches[i], H, pos0)
-            x = G.gemm_nt(y, bf(a.c_proj.weight), bias=bf(a.c_proj.bias), epi="resid", resid=x)
+                y = C.attention_decode(qkv, self.caches[i], H, pos0, pos_dev)
+            x = lin(y, a.c_proj.weight, a.c_proj.bias, "resid", resid=x)
             h2, _, _ = C.layernorm_fwd(x, bf(blk.ln_2.weight), bf(blk.ln_2.bias), eps)
-            pre = torch.empty((x.shape[0], 4 * D), dtype=torch.bfloat16, device=x.device)
-            u = G.gemm_nt(h2, bf(mm.c_fc.weight), bias=bf(mm.c_fc.bias), epi="gelu", pre_out=pre)
-            x = G.gemm_nt(u, bf(mm.c_proj.weight), bias=bf(mm.c_proj.bias), epi="resid", resid=x)
+            u = lin(h2, mm.c_fc.weight, mm.c_fc.bias, "gelu")
+            x = lin(u, mm.c_proj.weight, mm.c_proj.bias, "resid", resid=x)
         last = x.view(B, T, D)[:, -1].contiguous()
         hf, _, _ = C.layernorm_fwd(last, bf(tr.ln_f.weight), bf(tr.ln_f.bias), eps)
         V = cfg.vocab_size
-        logits = G.gemm_nt(hf, bf(m.lm_head.weight), ld=(V + 7) // 8 * 8)
+        logits = lin(hf, m.lm_head.weight, None, "none", ld=(V + 7) // 8 * 8)
         return logits[:, :V]
 
     def step(self, tok, pos):
-        return self._run(tok, pos)
+        """One decode step.  Decoding is launch-bound (B rows through ~10 kernels per layer), so
+        the step is captured once as a hipGraph over static token / position buffers and
+        replayed; the KV caches are persistent buffers the captured kernels append to."""
+        if not _GRAPH_DECODE:
+            return self._run(tok, pos)
+        g = getattr(self, "_graph", None)
+        if g is None:
+            g = self._graph = {"tok": tok.clone(), "pos": torch.full((1,), pos, dtype=torch.int32,
+                                                                     device=tok.device)}
+            self._run(g["tok"], pos, g["pos"])  # warm-up (workspaces, lazy kernel attributes)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                g["logits"] = self._run(g["tok"], max(pos, 1), g["pos"])
+            g["graph"] = graph
+        g["tok"].copy_(tok)
+        g["pos"].fill_(pos)
+        g["graph"].replay()
+        return g["logits"]
+
+
+_GRAPH_DECODE = True  # set False to launch the decode step eagerly
 
 
 @torch.no_grad()

@@ -158,3 +158,20 @@ def test_elementwise():
     dx2 = C.dropout_bias_grad(dy, db2, 0.5, 7)
     torch.testing.assert_close(dx2.float(), dx.float())
     torch.testing.assert_close(db2, dx.float().sum(0), atol=2e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("B,N,K", [(1, 2304, 768), (3, 768, 3072), (8, 50257, 768), (5, 100, 64)])
+def test_gemv_epilogues(B, N, K):
+    """Decode-time skinny GEMM (gemv.hip) vs fp32 torch for every epilogue."""
+    C = ext()
+    x, w, b = _bf(B, K, seed=21), _bf(N, K, scale=0.05, seed=22), _bf(N, seed=23)
+    ref = x.float() @ w.float().t()
+    ld = (N + 7) // 8 * 8
+    y0 = C.gemv(x, w, 0, None, None, ld)
+    _close(y0[:, :N], ref, atol=2e-2)
+    _close(C.gemv(x, w, 1, b, None, 0), ref + b.float(), atol=2e-2)
+    z = ref + b.float()
+    _close(C.gemv(x, w, 2, b, None, 0), 0.5 * z * (1 + torch.tanh(0.7978845608 * (z + 0.044715 * z ** 3))),
+           atol=2e-2)
+    r = _bf(B, N, seed=24)
+    _close(C.gemv(x, w, 3, b, r, 0), z + r.float(), atol=3e-2)

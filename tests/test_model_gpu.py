@@ -89,6 +89,22 @@ def test_generate_cache_matches_no_cache():
     assert c.shape == (2, 80)
 
 
+def test_generate_graph_decode_matches_eager(monkeypatch):
+    """The hipGraph-replayed decode step (device-side position) == the eagerly launched one."""
+    from mingpt_distributed_amd.models import generation as gen
+
+    torch.manual_seed(0)
+    model = GPT(_cfg(block_size=64), verbose=False).cuda().to(torch.bfloat16).eval()
+    idx = torch.randint(0, 1000, (3, 7), device="cuda")
+    monkeypatch.setattr(gen, "_GRAPH_DECODE", False)
+    a = model.generate(idx, 40, do_sample=False)
+    monkeypatch.setattr(gen, "_GRAPH_DECODE", True)
+    b = model.generate(idx, 40, do_sample=False)
+    assert torch.equal(a, b)
+    c = model.generate(idx, 80, do_sample=True, top_k=5)  # window slides: graph re-captured
+    assert c.shape == (3, 87)
+
+
 def test_gpt2_shape_step():
     """Full GPT-2 layer shapes (D=768, H=12, hd=64) at a short sequence through the engine."""
     torch.manual_seed(0)
