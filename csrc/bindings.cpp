@@ -366,7 +366,8 @@ at::Tensor attention_bwd(const at::Tensor& qkv, const at::Tensor& out, const at:
 
 // y[B, ldy] (ldy >= N) = epi(x[B, K] @ W[N, K]^T): the decode-time projection (gemv.hip)
 at::Tensor gemv(const at::Tensor& x, const at::Tensor& W, int64_t epi, const c10::optional<at::Tensor>& bias,
-                const c10::optional<at::Tensor>& resid, int64_t ldy) {
+                const c10::optional<at::Tensor>& resid, int64_t ldy, const c10::optional<at::Tensor>& lnw,
+                const c10::optional<at::Tensor>& lnb, double eps) {
   CHECK_BF16(x); CHECK_BF16(W); CHECK_CONTIG(x); CHECK_CONTIG(W);
   const int64_t K = W.size(1), N = W.size(0), B = x.numel() / K;
   TORCH_CHECK(x.size(-1) == K && mg::gemv_supported((int)B, (int)K), "gemv: B <= 8, K % 8 == 0, K <= 4096");
@@ -378,10 +379,15 @@ at::Tensor gemv(const at::Tensor& x, const at::Tensor& W, int64_t epi, const c10
     CHECK_BF16(*resid); CHECK_CONTIG(*resid);
     TORCH_CHECK(resid->numel() == B * ldy, "gemv: resid shape");
   }
+  TORCH_CHECK(lnw.has_value() == lnb.has_value(), "gemv: LayerNorm needs weight and bias");
+  if (lnw.has_value()) {
+    CHECK_BF16(*lnw); CHECK_BF16(*lnb);
+    TORCH_CHECK(lnw->numel() == K && lnb->numel() == K, "gemv: LayerNorm size");
+  }
   DevGuard g(x.device());
   auto y = at::empty({B, ldy}, x.options());
   mg::gemv(bp(x), bp(W), bp(y), (int)B, (int)N, (int)K, ldy, bias.has_value() ? bp(*bias) : nullptr,
-           epi == 3 ? bp(*resid) : nullptr, (int)epi, cur_stream());
+           epi == 3 ? bp(*resid) : nullptr, (int)epi, cur_stream(), bp_opt(lnw), bp_opt(lnb), (float)eps);
   return y;
 }
 
@@ -392,7 +398,7 @@ at::Tensor attention_decode(const at::Tensor& qkv_new, const at::Tensor& cache, 
   TORCH_CHECK(cache.dim() == 3, "cache must be [B, Tmax, 3D]");
   const int64_t B = cache.size(0), Tmax = cache.size(1), D3 = cache.size(2), D = D3 / 3;
   TORCH_CHECK(qkv_new.numel() == B * D3 && D % H == 0, "attention_decode: shape mismatch");
-  TORCH_CHECK(pos >= 0 && pos < Tmax && (D / H) % 8 == 0, "attention_decode: pos / head dim");
+  TORCH_CHECK(pos >= 0 && pos < Tmax && (D / H) % 8 == 0 && D / H <= 64, "attention_decode: pos / head dim");
   DevGuard g(cache.device());
   auto out = at::empty({B, D}, cache.options());
   const int* pd = nullptr;
@@ -435,7 +441,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attention_fwd", &attention_fwd);
   m.def("attention_bwd", &attention_bwd);
   m.def("gemv", &gemv, py::arg("x"), py::arg("W"), py::arg("epi"), py::arg("bias") = py::none(),
-        py::arg("resid") = py::none(), py::arg("ldy") = 0);
+        py::arg("resid") = py::none(), py::arg("ldy") = 0, py::arg("lnw") = py::none(),
+        py::arg("lnb") = py::none(), py::arg("eps") = 1e-5);
   m.def("gemv_supported", &mg::gemv_supported);
   m.def("attention_decode", &attention_decode, py::arg("qkv_new"), py::arg("cache"), py::arg("H"),
         py::arg("pos"), py::arg("pos_dev") = py::none());

@@ -45,7 +45,8 @@ void f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t stream);
 // gemv.hip (decode-time skinny GEMM, B <= 8 rows; epi 0 none, 1 bias, 2 bias+GELU, 3 bias+residual)
 bool gemv_supported(int B, int K);
 void gemv(const bf16_t* x, const bf16_t* W, bf16_t* y, int B, int N, int K, long ldy, const bf16_t* bias,
-          const bf16_t* resid, int epi, hipStream_t stream);
+          const bf16_t* resid, int epi, hipStream_t stream, const bf16_t* lnw = nullptr,
+          const bf16_t* lnb = nullptr, float eps = 1e-5f);
 
 // elementwise.hip
 void bias_act_fwd(const bf16_t* x, const bf16_t* b, bf16_t* pre, bf16_t* y, long M, int N, int act,

@@ -901,11 +901,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
                                                           const int* __restrict__ pos_dev,
                                                           float scale_log2) {
   if (pos_dev) pos = min(max(*pos_dev, 0), (int)Tmax - 1);  // hipGraph decode: position in device memory
-  extern __shared__ __attribute__((aligned(16))) float dsm[];  // [64 q][Tmax scores][4*64 acc][8]
+  extern __shared__ __attribute__((aligned(16))) float dsm[];  // [64 q][Tmax scores][32*64 acc][8]
   float* qs = dsm;
   float* sc = dsm + 64;
   float* acc = sc + ((Tmax + 3) & ~3L);
-  float* red = acc + 4 * 64;
+  float* red = acc + 32 * 64;
   const int b = blockIdx.x / H, hh = blockIdx.x % H;
   const long ld = 3L * D;
   const bf16_t* qrow = qkv_new + (long)b * ld + hh * hd;
@@ -940,19 +940,27 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   }
   sm = block_sum<4>(sm, red + 4);
   __syncthreads();
-  const int grp = threadIdx.x >> 6, d = threadIdx.x & 63;
-  float o = 0.f;
-  if (d < hd) {
-    for (int j = grp; j < L; j += 4) {
+  // P V: 32 key groups x 8 lanes of 8 dims (16-byte V loads), folded through LDS
+  const int grp = threadIdx.x >> 3, d8 = (threadIdx.x & 7) * 8;
+  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (d8 < hd) {
+    for (int j = grp; j < L; j += 32) {
       const bf16_t* vr = (j == pos) ? qrow + 2 * D : cb + (long)j * ld + 2 * D + hh * hd;
-      o += sc[j] * bf2f(vr[d]);
+      float v8[8];
+      unpack8(ld16(vr + d8), v8);
+      const float p = sc[j];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] += p * v8[e];
     }
   }
-  acc[grp * 64 + d] = o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[grp * 64 + d8 + e] = o[e];
   __syncthreads();
   if (threadIdx.x < hd) {
-    const float v = (acc[threadIdx.x] + acc[64 + threadIdx.x] + acc[128 + threadIdx.x] + acc[192 + threadIdx.x]) / sm;
-    out[(long)b * D + hh * hd + threadIdx.x] = f2bf(v);
+    float v = 0.f;
+#pragma unroll 8
+    for (int g = 0; g < 32; ++g) v += acc[g * 64 + threadIdx.x];
+    out[(long)b * D + hh * hd + threadIdx.x] = f2bf(v / sm);
   }
 }
 
@@ -962,7 +970,7 @@ namespace mg {
 
 void attention_decode(const bf16_t* qkv_new, bf16_t* cache, bf16_t* out, int B, int H, int hd,
                       long Tmax, int pos, hipStream_t stream, const int* pos_dev) {
-  const size_t smem = sizeof(float) * (64 + ((Tmax + 3) & ~3L) + 4 * 64 + 8);
+  const size_t smem = sizeof(float) * (64 + ((Tmax + 3) & ~3L) + 32 * 64 + 8);
   attn_decode_kernel<<<B * H, 256, smem, stream>>>(qkv_new, cache, out, H, hd, H * hd, Tmax, pos,
                                                    pos_dev, 1.4426950408889634f / sqrtf((float)hd));
 }

@@ -6,7 +6,8 @@
 // 6-24 workgroups walk a K loop one tile at a time and the projection is latency-bound
 // (26 us for the 3072 -> 768 MLP projection at B = 1).  The work is a stream of the weight
 // matrix (K x N bf16, read once) against B vectors that fit in LDS, so here:
-//   * x [B, K] is staged once per workgroup in LDS;
+//   * x [B, K] is staged once per workgroup in LDS -- optionally LayerNorm'ed on the way in (the
+//     LN that precedes every decode projection but the residual ones; one kernel instead of two);
 //   * a wave owns 4 output columns n: lanes 16g..16g+15 read row n = W[n, :] in 16-byte chunks
 //     (4 x 256 B contiguous segments per wave-instruction, 4 loads in flight per lane), FMA
 //     against the B vectors from LDS;
@@ -28,11 +29,49 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ x,
                                                    const bf16_t* __restrict__ W,
                                                    bf16_t* __restrict__ y, int N, int K, long ldy,
                                                    const bf16_t* __restrict__ bias,
-                                                   const bf16_t* __restrict__ resid, int epi) {
+                                                   const bf16_t* __restrict__ resid, int epi,
+                                                   const bf16_t* __restrict__ lnw,
+                                                   const bf16_t* __restrict__ lnb, float eps) {
   extern __shared__ __attribute__((aligned(16))) bf16_t xs[];  // [B][K]
-  for (int i = threadIdx.x * 8; i < B * K; i += 256 * 8) st16(xs + i, ld16(x + i));
-  __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lnw) {
+    // fused LayerNorm of the B input rows (wave w normalises rows w, w+4): the same lane/chunk
+    // order and wave reduction as ln_fwd_kernel, so the staged bf16 rows equal its output
+    for (int b = wid; b < B; b += 4) {
+      const bf16_t* xr = x + (long)b * K;
+      float s = 0.f;
+      for (int c = lane * 8; c < K; c += 512) {
+        float v[8];
+        unpack8(ld16(xr + c), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += v[e];
+      }
+      const float mu = wave_sum(s) / K;
+      float ss = 0.f;
+      for (int c = lane * 8; c < K; c += 512) {
+        float v[8];
+        unpack8(ld16(xr + c), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = v[e] - mu;
+          ss += d * d;
+        }
+      }
+      const float rs = rsqrtf(wave_sum(ss) / K + eps);
+      for (int c = lane * 8; c < K; c += 512) {
+        float v[8], wf[8], bf[8], o[8];
+        unpack8(ld16(xr + c), v);
+        unpack8(ld16(lnw + c), wf);
+        unpack8(ld16(lnb + c), bf);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (v[e] - mu) * rs * wf[e] + bf[e];
+        st16(xs + b * K + c, pack8(o));
+      }
+    }
+  } else {
+    for (int i = threadIdx.x * 8; i < B * K; i += 256 * 8) st16(xs + i, ld16(x + i));
+  }
+  __syncthreads();
   const int g = lane >> 4, j = lane & 15;  // 4 rows per wave, 16 lanes (256 B) per row segment
   const int n = (blockIdx.x * 4 + wid) * 4 + g;
   float acc[B];
@@ -94,11 +133,14 @@ namespace mg {
 bool gemv_supported(int B, int K) { return B >= 1 && B <= kGemvMaxB && K % 8 == 0 && K <= kGemvMaxK; }
 
 void gemv(const bf16_t* x, const bf16_t* W, bf16_t* y, int B, int N, int K, long ldy, const bf16_t* bias,
-          const bf16_t* resid, int epi, hipStream_t stream) {
+          const bf16_t* resid, int epi, hipStream_t stream, const bf16_t* lnw, const bf16_t* lnb,
+          float eps) {
   const int grid = cdiv(N, 16);  // 4 waves x 4 rows
   const size_t smem = sizeof(bf16_t) * (size_t)B * K;
 #define MG_GEMV_CASE(b) \
-  case b: gemv_kernel<b><<<grid, 256, smem, stream>>>(x, W, y, N, K, ldy, bias, resid, epi); break;
+  case b:                                                                                      \
+    gemv_kernel<b><<<grid, 256, smem, stream>>>(x, W, y, N, K, ldy, bias, resid, epi, lnw, lnb, eps); \
+    break;
   switch (B) {  // exact row counts: the kernel stages and writes exactly B rows
     MG_GEMV_CASE(1) MG_GEMV_CASE(2) MG_GEMV_CASE(3) MG_GEMV_CASE(4)
     MG_GEMV_CASE(5) MG_GEMV_CASE(6) MG_GEMV_CASE(7) MG_GEMV_CASE(8)

@@ -119,10 +119,15 @@ class _GpuCache:
         # one row tile and walks K latency-bound; prefill uses the MFMA GEMM
         skinny = pos0 > 0 and C.gemv_supported(B * T, 4 * D)
 
-        def lin(inp, w, b, epi, resid=None, ld=0):
+        def lin(inp, w, b, epi, resid=None, ld=0, ln=None):
+            """epi(LN(inp) @ w^T + b) with ``ln`` = a LayerNorm module applied first (fused into
+            the skinny GEMM's staging at decode time)."""
             if skinny:
                 code = {"none": 0, "bias": 1, "gelu": 2, "resid": 3}[epi]
-                return C.gemv(inp, bf(w), code, bf(b) if b is not None else None, resid, ld)
+                lw, lb = (bf(ln.weight), bf(ln.bias)) if ln is not None else (None, None)
+                return C.gemv(inp, bf(w), code, bf(b) if b is not None else None, resid, ld, lw, lb, eps)
+            if ln is not None:
+                inp, _, _ = C.layernorm_fwd(inp, bf(ln.weight), bf(ln.bias), eps)
             if epi == "gelu":
                 pre = torch.empty((inp.shape[0], w.shape[0]), dtype=torch.bfloat16, device=inp.device)
                 return G.gemm_nt(inp, bf(w), bias=bf(b), epi="gelu", pre_out=pre)
@@ -131,21 +136,18 @@ class _GpuCache:
 
         for i, blk in enumerate(tr.h):
             a, mm = blk.attn, blk.mlp
-            h, _, _ = C.layernorm_fwd(x, bf(blk.ln_1.weight), bf(blk.ln_1.bias), eps)
-            qkv = lin(h, a.c_attn.weight, a.c_attn.bias, "bias")
+            qkv = lin(x, a.c_attn.weight, a.c_attn.bias, "bias", ln=blk.ln_1)
             if pos0 == 0:
                 self.caches[i][:, :T].copy_(qkv.view(B, T, 3 * D))
                 y, _, _ = C.attention_fwd(qkv, B, T, H, 0.0, 0)
             else:
                 y = C.attention_decode(qkv, self.caches[i], H, pos0, pos_dev)
             x = lin(y, a.c_proj.weight, a.c_proj.bias, "resid", resid=x)
-            h2, _, _ = C.layernorm_fwd(x, bf(blk.ln_2.weight), bf(blk.ln_2.bias), eps)
-            u = lin(h2, mm.c_fc.weight, mm.c_fc.bias, "gelu")
+            u = lin(x, mm.c_fc.weight, mm.c_fc.bias, "gelu", ln=blk.ln_2)
             x = lin(u, mm.c_proj.weight, mm.c_proj.bias, "resid", resid=x)
         last = x.view(B, T, D)[:, -1].contiguous()
-        hf, _, _ = C.layernorm_fwd(last, bf(tr.ln_f.weight), bf(tr.ln_f.bias), eps)
         V = cfg.vocab_size
-        logits = lin(hf, m.lm_head.weight, None, "none", ld=(V + 7) // 8 * 8)
+        logits = lin(last, m.lm_head.weight, None, "none", ld=(V + 7) // 8 * 8, ln=tr.ln_f)
         return logits[:, :V]
 
     def step(self, tok, pos):

@@ -175,3 +175,8 @@ def test_gemv_epilogues(B, N, K):
            atol=2e-2)
     r = _bf(B, N, seed=24)
     _close(C.gemv(x, w, 3, b, r, 0), z + r.float(), atol=3e-2)
+    # fused LayerNorm staging == layernorm_fwd then the plain skinny GEMM (same rounding points)
+    lw, lb = _bf(K, seed=25) * 0.1 + 1, _bf(K, seed=26) * 0.1
+    h, _, _ = C.layernorm_fwd(x, lw, lb, 1e-5)
+    torch.testing.assert_close(C.gemv(x, w, 1, b, None, 0, lw, lb, 1e-5), C.gemv(h, w, 1, b, None, 0),
+                               atol=1e-2, rtol=1e-2)
