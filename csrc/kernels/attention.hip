@@ -803,13 +803,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
     if (kh ? act1 : act0) {
       // rows kh*128 + 16 kk + 8 h32 + q (+4): the 16 kk part is an immediate
       const int da = tr_off(8 * h32 + trq, qs * 32 + trc), db = tr_off(8 * h32 + 4 + trq, qs * 32 + trc);
-      const int ka = tr_off(8 * h32 + trq, dblk * 32 + trc), kb = tr_off(8 * h32 + 4 + trq, dblk * 32 + trc);
+      const int ko = tr_off(8 * h32 + trq, dblk * 32 + trc), ko4 = tr_off(8 * h32 + 4 + trq, dblk * 32 + trc);
       const char* sdSh = sdS + kh * 128 * ROWB;
       const char* sKh = sK + kh * 128 * ROWB;
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk)
         dq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_at(sdSh + kk * 16 * ROWB, da, db),
-                                                     lds_tr_at(sKh + kk * 16 * ROWB, ka, kb), dq, 0, 0, 0);
+                                                     lds_tr_at(sKh + kk * 16 * ROWB, ko, ko4), dq, 0, 0, 0);
     }
     float* part = reinterpret_cast<float*>(smem + B2_P) + tile * 4 * 64 * 4;
     if (kh == 1 && act1) {

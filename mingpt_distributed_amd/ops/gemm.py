@@ -30,6 +30,8 @@ def _row_chunks(M: int, *row_bytes: int):
     ``row_bytes`` wide reaches 4 GiB (e.g. GPT-2 logits at > 42k tokens per GPU): the M-chunked
     launches are exact (the epilogues used here do not depend on the global row index)."""
     cap = max(256, (_MAX_BYTES // max(max(row_bytes), 1)) // 256 * 256)
+    if M <= cap:
+        return [(0, M)]
     n = -(-M // cap)
     step = min(cap, -(-(-(-M // n)) // 256) * 256)  # balanced: equal tile counts per launch
     return [(r0, min(M, r0 + step)) for r0 in range(0, M, step)]
