@@ -831,11 +831,17 @@ __global__ __launch_bounds__(512, 1) void attn_bwd256_kernel(const AttnArgs a) {
       // attn_dq_finalize sums the partials of key blocks kb0 <= q), no atomics, no memset
       const int d = dblk * 32 + l32;
       if (d < a.hd) {
-        float* dqb = a.dq + kb * a.dq_part + ((long)b * a.T) * a.D + hh * a.hd + d;
+        // row q0 + (r & 3) + 8 (r >> 2): one 64-bit base per lane, then uniform row strides
+        const int q0 = qbase + qs * 32 + 4 * h32;
+        float* dqb = a.dq + kb * a.dq_part + ((long)b * a.T + q0) * a.D + hh * a.hd + d;
+        const long rs = a.D;
+        if (qbase + BQ <= a.T) {  // whole tile inside the sequence: no per-row checks
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int q = qbase + qs * 32 + (r & 3) + 8 * (r >> 2) + 4 * h32;
-          if (q < a.T) dqb[(long)q * a.D] = dq[r];
+          for (int r = 0; r < 16; ++r) dqb[((r & 3) + 8 * (r >> 2)) * rs] = dq[r];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (q0 + (r & 3) + 8 * (r >> 2) < a.T) dqb[((r & 3) + 8 * (r >> 2)) * rs] = dq[r];
         }
       }
     }
