@@ -32,6 +32,32 @@ def _bf16(t: torch.Tensor) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------------------------ embedding
+
+# Plain GEMMs of the block (no fused epilogue) run on the library GEMM (hipBLASLt via torch.mm /
+# torch.addmm): the three epilogue-free data gradients (qkv, attention projection, MLP fc) and the
+# qkv projection, whose bias epilogue hipBLASLt fuses too.  One-box A/B at B=64: +1.0 % for the
+# dgrads, +0.5 % for qkv, +1.7 % together (920k -> 935k tok/s); hipBLASLt's main loop is ~20 %
+# faster than W4's at K >= 1536 (bench/gemm_ksweep.py) and these GEMMs have nothing to fuse.  The
+# weight gradients stay on gemm.hip (fp32 accumulate; the fp32-out library GEMM + add was 13 %
+# slower per step), as do the GELU / residual-dropout / GELU' epilogue GEMMs.
+_DGRAD_BLAS = os.environ.get("MINGPT_DGRAD_BLAS", "1") == "1"
+_WGRAD_BLAS = os.environ.get("MINGPT_WGRAD_BLAS", "0") == "1"
+_QKV_BLAS = os.environ.get("MINGPT_QKV_BLAS", "1") == "1"
+
+
+def _dgrad(dy, w):
+    """dX = dY @ W for a plain (epilogue-free) data gradient."""
+    return torch.mm(dy, w) if _DGRAD_BLAS else G.gemm_dgrad(dy, w)
+
+
+def _wgrad(dy, x, main_grad):
+    """main_grad += dY^T @ X (fp32)."""
+    if _WGRAD_BLAS:
+        main_grad.add_(torch.mm(dy.t(), x, out_dtype=torch.float32))
+    else:
+        G.gemm_tn_acc(dy, x, main_grad)
+
+
 class EmbeddingFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, idx, wte, wpe, p):
@@ -65,7 +91,7 @@ class TransformerBlockFn(torch.autograd.Function):
         seeds = (new_seed() if p_attn > 0 else 0, new_seed() if p_resid > 0 else 0,
                  new_seed() if p_resid > 0 else 0)
         h, mean1, rstd1 = C.layernorm_fwd(x, ln1w, ln1b, eps)
-        qkv = G.gemm_nt(h, wqkv, bias=bqkv, epi="bias")
+        qkv = torch.addmm(bqkv, h, wqkv.t()) if _QKV_BLAS else G.gemm_nt(h, wqkv, bias=bqkv, epi="bias")
         y, lse, amask = C.attention_fwd(qkv, B, T, H, float(p_attn), seeds[0])
         x1 = G.gemm_nt(y, wo, bias=bo, epi="resid", resid=x, p=p_resid, seed=seeds[1])
         h2, mean2, rstd2 = C.layernorm_fwd(x1, ln2w, ln2b, eps)
@@ -95,11 +121,11 @@ class TransformerBlockFn(torch.autograd.Function):
         else:
             dz = dx2
             C.bias_grad(dz, g[id(bp)][0])
-        G.gemm_tn_acc(dz, u, g[id(wp)][0])
+        _wgrad(dz, u, g[id(wp)][0])
         dpre = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=gd)
-        G.gemm_tn_acc(dpre, h2, g[id(wfc)][0])
+        _wgrad(dpre, h2, g[id(wfc)][0])
         C.bias_grad(dpre, g[id(bfc)][0])  # separate pass: cheaper than column sums in the epilogue
-        dh2 = G.gemm_dgrad(dpre, wfc)
+        dh2 = _dgrad(dpre, wfc)
         dx1 = C.layernorm_bwd(dh2, x1, ln2w, mean2, rstd2, g[id(ln2w)][0], g[id(ln2b)][0], dx2)
         # ---- attention: x1 = x + drop(attn(h Wqkv^T + bqkv) Wo^T + bo)
         if p_resid > 0:
@@ -107,12 +133,12 @@ class TransformerBlockFn(torch.autograd.Function):
         else:
             dz = dx1
             C.bias_grad(dz, g[id(bo)][0])
-        G.gemm_tn_acc(dz, y, g[id(wo)][0])
-        dy = G.gemm_dgrad(dz, wo)
+        _wgrad(dz, y, g[id(wo)][0])
+        dy = _dgrad(dz, wo)
         dqkv = C.attention_bwd(qkv, y, dy, lse, amask, B, T, H, float(p_attn), ctx.seeds[0])
-        G.gemm_tn_acc(dqkv, h, g[id(wqkv)][0])
+        _wgrad(dqkv, h, g[id(wqkv)][0])
         C.bias_grad(dqkv, g[id(bqkv)][0])
-        dh = G.gemm_dgrad(dqkv, wqkv)
+        dh = _dgrad(dqkv, wqkv)
         dx = C.layernorm_bwd(dh, x, ln1w, mean1, rstd1, g[id(ln1w)][0], g[id(ln1b)][0], dx1)
         outs = [finish(prm, *g[id(prm)]) for prm in ctx.params]
         return (dx, *outs, None)
