@@ -909,6 +909,17 @@ struct W4 {
   static constexpr int NR = 8 + FN;                   // fragment reads / DMA pieces per phase
 };
 
+// DMA piece issued after MFMA q of phase B (or -1): the NR pieces spread evenly over the NQ MFMAs.
+// The CU's LDS-DMA path moves ~64 B/clk, so one K-tile's 64 KiB take ~1k cycles -- half the K-tile's
+// MFMA time; bunched into the first half of the phase (one per 2 MFMAs) the pieces out-ran it and
+// stalled the in-order MFMA stream behind them (stamped: phase B 1.7-1.9k cycles vs phase A 1.08k).
+template <int NQ, int NR>
+MG_DEVICE constexpr int w4_piece_at(int q) {
+  for (int r = 0; r < NR; ++r)
+    if (r * NQ / NR == q) return r;
+  return -1;
+}
+
 // the K-loop's final MFMA with the wait states its result needs before any VALU / scratch read
 // (hipcc cannot see the latency of an asm MFMA; whatever it places after the loop -- epilogue reads,
 // spill stores -- must not start inside that window)
@@ -940,6 +951,17 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
   const int m0 = (first_m + (wg % group) % gm) * 256;
   const int n0 = ((wg % group) / gm) * BN;
 
+#ifdef MG_GEMM_STAMPS
+  // diagnostic builds: [0..5] segments of K-tile MG_GEMM_STAMPS (phase A issue | wait | barrier |
+  // phase B | fragment wait), [6..9] kernel start | main loop start | main loop end | end
+  unsigned long long st[10];
+#define W4_STAMP(k) st[k] = __builtin_amdgcn_s_memtime()
+#define W4_KSTAMP(k) if (kt == MG_GEMM_STAMPS) st[k] = __builtin_amdgcn_s_memtime()
+#else
+#define W4_STAMP(k)
+#define W4_KSTAMP(k)
+#endif
+  W4_STAMP(6);
   f32x4 acc[8][FN];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -971,8 +993,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
   for (int i = 0; i < 8; ++i) fa0[i] = frag<AK>(smem, wm * 8 + i, 0, lane);
   lds_ready(fa0);
   lds_ready(fb0, false);
+  W4_STAMP(7);
 
   for (int kt = 0; kt < nk; ++kt) {
+    W4_KSTAMP(0);
     const char* sa = smem + (kt & 1) * WK::STAGE;
     // phase A: k32 step 0 of tile kt; step-1 fragments read between the MFMAs (one per 2)
 #pragma unroll
@@ -987,11 +1011,14 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
       }
     }
     // tile kt+1 landed (this wave's DMA), every wave done reading buffer kt & 1
+    W4_KSTAMP(1);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     lds_ready(fa1, false);
     lds_ready(fb1, false);
+    W4_KSTAMP(2);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    W4_KSTAMP(3);
     // phase B: k32 step 1 of tile kt; DMA of tile kt+2 into buffer kt & 1 (or the sink) and the
     // step-0 fragments of tile kt+1 between the MFMAs
     const int t2 = kt + 2;
@@ -1006,8 +1033,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
       // duplicate the accumulator into other AGPRs; 16 cycles per 2048 is cheaper than that)
       if (q == NQ - 1) mfma_acc_last(acc[i][j], fb1[j], fa1[i]);
       else mfma_acc(acc[i][j], fb1[j], fa1[i]);
-      if (q < 2 * NR && (q & 1) == 0) {
-        const int r = q >> 1;  // DMA pieces: 8 of A, FN of B
+      if (w4_piece_at<NQ, NR>(q) >= 0) {
+        const int r = w4_piece_at<NQ, NR>(q);  // DMA pieces: 8 of A, FN of B
         if (r < 8) sta.piece(dst, ra, tt, r);
         else stb.piece(t2 < nk ? dst + CF::A_BYTES : dst, rb, tt, r - 8);
       }
@@ -1019,12 +1046,23 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
         else fa0[r - FN] = frag<AK>(sn, wm * 8 + r - FN, 0, lane);
       }
     }
+    W4_KSTAMP(4);
     lds_ready(fa0);  // read early in phase B: long landed, the wait is free
     lds_ready(fb0, false);
+    W4_KSTAMP(5);
   }
+  W4_STAMP(8);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
   epilogue<CF, EPI, OUTF32, WK::SMEM / 4>(args, acc, m0, n0, wm, wn, wid, lane, smem);
+#ifdef MG_GEMM_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stores drained
+  W4_STAMP(9);
+  if (args.dbg && lane == 0)
+    for (int k = 0; k < 10; ++k) args.dbg[((long)blockIdx.x * 8 + wid) * 24 + k] = st[k];
+#endif
+#undef W4_STAMP
+#undef W4_KSTAMP
 }
 
 template <int BN, bool AK, bool BKC, int EPI, bool OUTF32>

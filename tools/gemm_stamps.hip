@@ -50,6 +50,32 @@ int main(int argc, char** argv) {
   hipDeviceSynchronize();
   std::vector<unsigned long long> h((size_t)blocks * 8 * 24);
   hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost);
+  if (variant == 5 || variant == 6) {  // W4: K-tile segments and per-tile prologue / loop / epilogue
+    const char* wseg[5] = {"phaseA", "wait", "barrier", "phaseB", "fragwait"};
+    auto med = [&](int k0, int k1) {
+      std::vector<long long> v;
+      for (int bl = 0; bl < blocks; ++bl)
+        for (int w = 0; w < 4; ++w) {
+          const unsigned long long* s = &h[((size_t)bl * 8 + w) * 24];
+          if (s[k0] && s[k1]) v.push_back((long long)(s[k1] - s[k0]));
+        }
+      std::sort(v.begin(), v.end());
+      return v.empty() ? -1LL : v[v.size() / 2];
+    };
+    printf("W4 K-tile %d, median cycles:", MG_GEMM_STAMPS);
+    for (int k = 0; k < 5; ++k) printf(" %s=%lld", wseg[k], med(k, k + 1));
+    printf("\nper tile: prologue=%lld main_loop=%lld epilogue=%lld (K-tiles %d)\n", med(6, 7), med(7, 8),
+           med(8, 9), K / 64);
+    // wall time per CU round: first start to last end over all blocks
+    unsigned long long lo = ~0ull, hi = 0;
+    for (int bl = 0; bl < blocks; ++bl) {
+      const unsigned long long* s = &h[(size_t)bl * 8 * 24];
+      if (s[6]) lo = std::min(lo, s[6]);
+      if (s[9]) hi = std::max(hi, s[9]);
+    }
+    printf("span %llu cycles for %d tiles\n", hi - lo, blocks);
+    return 0;
+  }
   const char* seg[6] = {"reads+dma", "vmcnt", "barrier1", "lgkmcnt", "mfma", "barrier2"};
   for (int grp = 0; grp < 2; ++grp) {
     printf("group %d (waves %d-%d), median cycles per segment:\n", grp, grp * 4, grp * 4 + 3);
