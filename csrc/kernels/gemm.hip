@@ -884,12 +884,20 @@ void launch_pp(GemmArgs a, hipStream_t stream) {
 // 4-wave 256x256 kernel ("W4"): one wave per SIMD, 128x128 wave tile (256 accumulator registers,
 // 512-register budget), the structure that keeps MFMA busy without a partner wave.
 //
-// Per K-tile kt (BK = 64 = two k32 steps, LDS buffer kt & 1, the T256 images):
-//   phase A: 64 MFMAs on the k32 step 0 fragments while the step-1 fragments are read
-//   s_waitcnt vmcnt(0) lgkmcnt(0) + barrier   (tile kt+1 has landed; buffer kt & 1 fully read)
-//   phase B: LDS-DMA of tile kt+2 into buffer kt & 1, step-0 fragments of tile kt+1 read, 64 MFMAs
-//            on the step-1 fragments
-// One barrier per K-tile; each tile's DMA has ~1.5 K-tiles of MFMA work to land in.
+// Per K-tile kt (BK = 64 = two k32 steps, the T256 images; A in a 2-slot LDS ring, slot kt & 1,
+// B in a 3-slot ring, slot kt % 3):
+//   phase A: 64 MFMAs on the k32 step-0 fragments; step-1 fragments of tile kt read; LDS-DMA of
+//            tile kt+2's B into B slot (kt+2) % 3 (it held tile kt-1, fully read before the
+//            previous K-tile's barrier)
+//   s_waitcnt vmcnt(B pieces) lgkmcnt(0) + barrier   (tile kt+1 landed; A slot kt & 1 fully read)
+//   phase B: 64 MFMAs on the step-1 fragments; step-0 fragments of tile kt+1 read; LDS-DMA of
+//            tile kt+2's A into A slot kt & 1
+// One barrier per K-tile, and the K-tile's DMA (64 KiB per CU, ~1k cycles of the CU's ~64 B/clk
+// LDS-DMA path) is split evenly over both phases, one piece per 8 MFMAs: issued in one phase it
+// out-ran the DMA path and stalled the in-order MFMA stream behind it (tools/gemm_stamps.hip:
+// phase B 1.94k cycles with the pieces bunched, 1.47k spread over phase B, phase A 1.08k).
+// The third B slot replaces the old DMA sink: DMA past the last K-tile re-reads tile 0 into
+// slots nobody reads again, so every K-tile waits with the same counts.
 // MFMA with the accumulator pinned to AGPRs ("+a"): with 256 accumulator registers the compiler's
 // own allocation shuffles them between AGPRs and VGPRs every K-step.  volatile + "memory" keeps
 // program order between the MFMAs and the LDS reads / DMA pieces placed between them: one wave per
@@ -903,16 +911,15 @@ MG_DEVICE void mfma_acc(f32x4& acc, const bf16x8& a, const bf16x8& b) {
 template <int BN>
 struct W4 {
   static constexpr int FN = BN / 32;                  // 16-col fragments per wave (2 x 2 waves)
-  static constexpr int STAGE = 32768 + BN * 128;      // one K-tile: A 32 KiB + B BN x 128 B
-  static constexpr int SINK = 2 * STAGE;              // DMA past the last K-tile lands here
-  static constexpr int SMEM = 2 * STAGE + 32768;
-  static constexpr int NR = 8 + FN;                   // fragment reads / DMA pieces per phase
+  static constexpr int A_SLOT = 32768;                // 256 x 64 bf16
+  static constexpr int B_SLOT = BN * 128;             // BN x 64 bf16
+  static constexpr int B_RING = 2 * A_SLOT;           // [A0][A1][B0][B1][B2]
+  static constexpr int SMEM = 2 * A_SLOT + 3 * B_SLOT;  // 160 KiB at BN = 256
+  static constexpr int NR = 8 + FN;                   // fragment reads per phase
+  static constexpr int PA = 8, PB = FN;               // DMA pieces per wave per K-tile (A, B)
 };
 
-// DMA piece issued after MFMA q of phase B (or -1): the NR pieces spread evenly over the NQ MFMAs.
-// The CU's LDS-DMA path moves ~64 B/clk, so one K-tile's 64 KiB take ~1k cycles -- half the K-tile's
-// MFMA time; bunched into the first half of the phase (one per 2 MFMAs) the pieces out-ran it and
-// stalled the in-order MFMA stream behind them (stamped: phase B 1.7-1.9k cycles vs phase A 1.08k).
+// DMA piece issued after MFMA q of a phase (or -1): NR pieces spread evenly over the NQ MFMAs.
 template <int NQ, int NR>
 MG_DEVICE constexpr int w4_piece_at(int q) {
   for (int r = 0; r < NR; ++r)
@@ -974,12 +981,13 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
   Stager<BKC, BN, 4> stb;
   sta.init(args.A, args.a_bytes, args.lda, m0, args.a_ext, kbeg, args.ka, kbeg + args.kchunk, wid, lane);
   stb.init(args.B, args.b_bytes, args.ldb, n0, args.b_ext, kbeg, args.kb, kbeg + args.kchunk, wid, lane);
+  char* const sB = smem + WK::B_RING;
   sta.stage(smem, 0);
-  stb.stage(smem + CF::A_BYTES, 0);
+  stb.stage(sB, 0);
   if (nk > 1) {
-    sta.stage(smem + WK::STAGE, 1);
-    stb.stage(smem + WK::STAGE + CF::A_BYTES, 1);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NR) : "memory");
+    sta.stage(smem + WK::A_SLOT, 1);
+    stb.stage(sB + WK::B_SLOT, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WK::PA + WK::PB) : "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -988,68 +996,78 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
 
   bf16x8 fa0[8], fb0[FN], fa1[8], fb1[FN];
 #pragma unroll
-  for (int j = 0; j < FN; ++j) fb0[j] = frag<BKC>(smem + CF::A_BYTES, wn * FN + j, 0, lane);
+  for (int j = 0; j < FN; ++j) fb0[j] = frag<BKC>(sB, wn * FN + j, 0, lane);
 #pragma unroll
   for (int i = 0; i < 8; ++i) fa0[i] = frag<AK>(smem, wm * 8 + i, 0, lane);
   lds_ready(fa0);
   lds_ready(fb0, false);
   W4_STAMP(7);
 
+  int bs = 0;  // B slot of tile kt (kt % 3)
   for (int kt = 0; kt < nk; ++kt) {
     W4_KSTAMP(0);
-    const char* sa = smem + (kt & 1) * WK::STAGE;
-    // phase A: k32 step 0 of tile kt; step-1 fragments read between the MFMAs (one per 2)
+    const int bs1 = bs == 2 ? 0 : bs + 1, bs2 = bs == 0 ? 2 : bs - 1;  // slots of kt+1, kt+2
+    const char* sa = smem + (kt & 1) * WK::A_SLOT;
+    const char* sb = sB + bs * WK::B_SLOT;
+    const int t2 = kt + 2;
+    const int tt = t2 < nk ? t2 : 0;  // past the end: re-read tile 0 into a slot nobody reads
+    // phase A: k32 step 0 of tile kt; step-1 fragments read between the MFMAs (one per 2); B of
+    // tile kt+2 by DMA into B slot (kt+2) % 3
+    {
+      const __amdgpu_buffer_rsrc_t rb = stb.rsrc(tt);
+      char* dstb = sB + bs2 * WK::B_SLOT;
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int i = q / FN, j = q % FN;
-      mfma_acc(acc[i][j], fb0[j], fa0[i]);
-      if ((q & 1) == 0 && q < 2 * NR) {
-        // B fragments first: the next phase's first FN MFMAs use fa[0] with every fb[j]
-        const int r = q >> 1;
-        if (r < FN) fb1[r] = frag<BKC>(sa + CF::A_BYTES, wn * FN + r, 1, lane);
-        else fa1[r - FN] = frag<AK>(sa, wm * 8 + r - FN, 1, lane);
+      for (int q = 0; q < NQ; ++q) {
+        const int i = q / FN, j = q % FN;
+        mfma_acc(acc[i][j], fb0[j], fa0[i]);
+        if ((q & 1) == 0 && q < 2 * NR) {
+          // B fragments first: the next phase's first FN MFMAs use fa[0] with every fb[j]
+          const int r = q >> 1;
+          if (r < FN) fb1[r] = frag<BKC>(sb, wn * FN + r, 1, lane);
+          else fa1[r - FN] = frag<AK>(sa, wm * 8 + r - FN, 1, lane);
+        }
+        if (w4_piece_at<NQ, WK::PB>(q) >= 0) stb.piece(dstb, rb, tt, w4_piece_at<NQ, WK::PB>(q));
       }
     }
-    // tile kt+1 landed (this wave's DMA), every wave done reading buffer kt & 1
+    // tile kt+1 landed (this wave's DMA older than the B pieces just issued), every wave done
+    // reading A slot kt & 1
     W4_KSTAMP(1);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(WK::PB) : "memory");
     lds_ready(fa1, false);
     lds_ready(fb1, false);
     W4_KSTAMP(2);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     W4_KSTAMP(3);
-    // phase B: k32 step 1 of tile kt; DMA of tile kt+2 into buffer kt & 1 (or the sink) and the
-    // step-0 fragments of tile kt+1 between the MFMAs
-    const int t2 = kt + 2;
-    const int tt = t2 < nk ? t2 : 0;
-    char* dst = t2 < nk ? smem + (kt & 1) * WK::STAGE : smem + WK::SINK;
-    const __amdgpu_buffer_rsrc_t ra = sta.rsrc(tt), rb = stb.rsrc(tt);
-    const char* sn = smem + ((kt + 1) & 1) * WK::STAGE;
+    // phase B: k32 step 1 of tile kt; A of tile kt+2 by DMA into A slot kt & 1; step-0 fragments
+    // of tile kt+1 between the MFMAs
+    {
+      const __amdgpu_buffer_rsrc_t ra = sta.rsrc(tt);
+      char* dsta = smem + (kt & 1) * WK::A_SLOT;
+      const char* sn = smem + ((kt + 1) & 1) * WK::A_SLOT;
+      const char* snb = sB + bs1 * WK::B_SLOT;
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int i = q / FN, j = q % FN;
-      // every K-tile's final MFMA carries the wait states (a branch on "last K-tile" makes hipcc
-      // duplicate the accumulator into other AGPRs; 16 cycles per 2048 is cheaper than that)
-      if (q == NQ - 1) mfma_acc_last(acc[i][j], fb1[j], fa1[i]);
-      else mfma_acc(acc[i][j], fb1[j], fa1[i]);
-      if (w4_piece_at<NQ, NR>(q) >= 0) {
-        const int r = w4_piece_at<NQ, NR>(q);  // DMA pieces: 8 of A, FN of B
-        if (r < 8) sta.piece(dst, ra, tt, r);
-        else stb.piece(t2 < nk ? dst + CF::A_BYTES : dst, rb, tt, r - 8);
-      }
-      if (q < 2 * NR && (q & 1) == 1) {
-        // fragment reads of tile kt+1 step 0, B first, interleaved with the DMA pieces early in the
-        // phase so they have ~3/4 of it to land before the next phase A needs them
-        const int r = q >> 1;
-        if (r < FN) fb0[r] = frag<BKC>(sn + CF::A_BYTES, wn * FN + r, 0, lane);
-        else fa0[r - FN] = frag<AK>(sn, wm * 8 + r - FN, 0, lane);
+      for (int q = 0; q < NQ; ++q) {
+        const int i = q / FN, j = q % FN;
+        // every K-tile's final MFMA carries the wait states (a branch on "last K-tile" makes hipcc
+        // duplicate the accumulator into other AGPRs; 16 cycles per 2048 is cheaper than that)
+        if (q == NQ - 1) mfma_acc_last(acc[i][j], fb1[j], fa1[i]);
+        else mfma_acc(acc[i][j], fb1[j], fa1[i]);
+        if (w4_piece_at<NQ, WK::PA>(q) >= 0) sta.piece(dsta, ra, tt, w4_piece_at<NQ, WK::PA>(q));
+        if (q < 2 * NR && (q & 1) == 1) {
+          // fragment reads of tile kt+1 step 0, B first, early in the phase so they have ~3/4 of
+          // it to land before the next phase A needs them
+          const int r = q >> 1;
+          if (r < FN) fb0[r] = frag<BKC>(snb, wn * FN + r, 0, lane);
+          else fa0[r - FN] = frag<AK>(sn, wm * 8 + r - FN, 0, lane);
+        }
       }
     }
     W4_KSTAMP(4);
     lds_ready(fa0);  // read early in phase B: long landed, the wait is free
     lds_ready(fb0, false);
     W4_KSTAMP(5);
+    bs = bs1;
   }
   W4_STAMP(8);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
