@@ -150,10 +150,12 @@ struct Stager {
   }
   // piece-level form for hand-interleaved schedules: descriptor once per tile, then piece(i)
   MG_DEVICE __amdgpu_buffer_rsrc_t rsrc(int t) const { return tile_rsrc(base, bytes, step, t); }
-  MG_DEVICE void piece(char* lds, __amdgpu_buffer_rsrc_t rs, int t, int i) const {
+  // check = false: no per-lane k check, full K-tiles only (W4 visits its one partial K-tile first,
+  // in the prologue)
+  MG_DEVICE void piece(char* lds, __amdgpu_buffer_rsrc_t rs, int t, int i, bool check = true) const {
     const int j = swid * PER + i;
     uint32_t off = voff[i];
-    if (t >= tail_t) {
+    if (check && t >= tail_t) {
       const int lane = threadIdx.x & 63;
       const int kpos = KC ? ((lane & 7) ^ ((lane >> 3) & 7)) * 8 : 4 * (j & 15) + (lane >> 4);
       off = kpos < klim - t * BK ? off : kOOB;
@@ -927,6 +929,9 @@ MG_DEVICE constexpr int w4_piece_at(int q) {
   return -1;
 }
 
+// K-tile visited s-th (tail_first: the partial last K-tile, then 0, 1, ...)
+MG_DEVICE int w4_tile(int s, int nk, bool tail_first) { return tail_first ? (s == 0 ? nk - 1 : s - 1) : s; }
+
 // the K-loop's final MFMA with the wait states its result needs before any VALU / scratch read
 // (hipcc cannot see the latency of an asm MFMA; whatever it places after the loop -- epilogue reads,
 // spill stores -- must not start inside that window)
@@ -981,12 +986,16 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
   Stager<BKC, BN, 4> stb;
   sta.init(args.A, args.a_bytes, args.lda, m0, args.a_ext, kbeg, args.ka, kbeg + args.kchunk, wid, lane);
   stb.init(args.B, args.b_bytes, args.ldb, n0, args.b_ext, kbeg, args.kb, kbeg + args.kchunk, wid, lane);
+  // K-tile visiting order: a partial last K-tile (K % 64 != 0; W4 layouts have ka = kb = K and
+  // split-K chunks of whole tiles, so it is the only tile needing per-lane k checks) goes first,
+  // staged in the prologue, so the main loop's DMA pieces carry no check (a v_cndmask each)
+  const bool tail_first = (sta.klim % BK) != 0;
   char* const sB = smem + WK::B_RING;
-  sta.stage(smem, 0);
-  stb.stage(sB, 0);
+  sta.stage(smem, w4_tile(0, nk, tail_first));
+  stb.stage(sB, w4_tile(0, nk, tail_first));
   if (nk > 1) {
-    sta.stage(smem + WK::A_SLOT, 1);
-    stb.stage(sB + WK::B_SLOT, 1);
+    sta.stage(smem + WK::A_SLOT, w4_tile(1, nk, tail_first));
+    stb.stage(sB + WK::B_SLOT, w4_tile(1, nk, tail_first));
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WK::PA + WK::PB) : "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1010,7 +1019,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
     const char* sa = smem + (kt & 1) * WK::A_SLOT;
     const char* sb = sB + bs * WK::B_SLOT;
     const int t2 = kt + 2;
-    const int tt = t2 < nk ? t2 : 0;  // past the end: re-read tile 0 into a slot nobody reads
+    const int tt = w4_tile(t2 < nk ? t2 : 1, nk, tail_first);  // past the end: re-read a tile into a slot nobody reads
     // phase A: k32 step 0 of tile kt; step-1 fragments read between the MFMAs (one per 2); B of
     // tile kt+2 by DMA into B slot (kt+2) % 3
     {
@@ -1026,7 +1035,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
           if (r < FN) fb1[r] = frag<BKC>(sb, wn * FN + r, 1, lane);
           else fa1[r - FN] = frag<AK>(sa, wm * 8 + r - FN, 1, lane);
         }
-        if (w4_piece_at<NQ, WK::PB>(q) >= 0) stb.piece(dstb, rb, tt, w4_piece_at<NQ, WK::PB>(q));
+        if (w4_piece_at<NQ, WK::PB>(q) >= 0) stb.piece(dstb, rb, tt, w4_piece_at<NQ, WK::PB>(q), false);
       }
     }
     // tile kt+1 landed (this wave's DMA older than the B pieces just issued), every wave done
@@ -1053,7 +1062,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
         // duplicate the accumulator into other AGPRs; 16 cycles per 2048 is cheaper than that)
         if (q == NQ - 1) mfma_acc_last(acc[i][j], fb1[j], fa1[i]);
         else mfma_acc(acc[i][j], fb1[j], fa1[i]);
-        if (w4_piece_at<NQ, WK::PA>(q) >= 0) sta.piece(dsta, ra, tt, w4_piece_at<NQ, WK::PA>(q));
+        if (w4_piece_at<NQ, WK::PA>(q) >= 0) sta.piece(dsta, ra, tt, w4_piece_at<NQ, WK::PA>(q), false);
         if (q < 2 * NR && (q & 1) == 1) {
           // fragment reads of tile kt+1 step 0, B first, early in the phase so they have ~3/4 of
           // it to land before the next phase A needs them
