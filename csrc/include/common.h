@@ -201,6 +201,19 @@ MG_DEVICE float gelu_grad_from(float x, float sg) {
 }
 MG_DEVICE float gelu_grad(float x) { return gelu_grad_from(x, gelu_sigmoid(x)); }
 
+// GELU and GELU' of two values with packed fp32 math (v_pk_mul_f32 / v_pk_fma_f32: two lanes'
+// worth per instruction; only exp2 and rcp stay per element).  Same formulas and rounding steps as
+// gelu_sigmoid / gelu_grad_from; used by the GEMM epilogue, where one wave per SIMD runs ~12 VALU
+// ops per element with nothing to overlap them.
+MG_DEVICE void gelu2(f32x2 x, f32x2& y, f32x2& g) {
+  const f32x2 x2 = x * x;
+  const f32x2 t = x * (kGeluE1 * x2 + kGeluE0);
+  const f32x2 d = f32x2{1.f, 1.f} + f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+  const f32x2 sg = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  y = x * sg;
+  g = (2.f * kGeluK0) * x * sg * (f32x2{1.f, 1.f} - sg) * ((3.f * kGeluK1) * x2 + 1.f) + sg;
+}
+
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace mg

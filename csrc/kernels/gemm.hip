@@ -337,16 +337,13 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
           v[2] += bf2f(bs[j].y & 0xffffu); v[3] += bf2f(bs[j].y >> 16);
         }
         const int col = j * 16 + (lane >> 4) * 4;
-        if constexpr (EPI == 2) {  // y = GELU(z); GELU'(z) into the second plane
-          float gd[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float sg = gelu_sigmoid(v[r]);
-            gd[r] = gelu_grad_from(v[r], sg);
-            v[r] *= sg;
-          }
+        if constexpr (EPI == 2) {  // y = GELU(z); GELU'(z) into the second plane (packed fp32 math)
+          f32x2 y0, y1, g0, g1;
+          gelu2(f32x2{v[0], v[1]}, y0, g0);
+          gelu2(f32x2{v[2], v[3]}, y1, g1);
+          v[0] = y0.x; v[1] = y0.y; v[2] = y1.x; v[3] = y1.y;
           *reinterpret_cast<uint2*>(row + CHF * 16 * S + col * 2) =
-              make_uint2(pack2(gd[0], gd[1]), pack2(gd[2], gd[3]));
+              make_uint2(pack2(g0.x, g0.y), pack2(g1.x, g1.y));
         }
         if constexpr (EPI == 3) {
           if (args.thr) {  // one Philox call per 64-column block of this lane's row (common.h rowdrop)
