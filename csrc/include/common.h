@@ -142,10 +142,12 @@ MG_DEVICE void dropout8(float (&v)[8], uint64_t seed, uint64_t e, uint32_t thr, 
 // ---------------------------------------------------------------- residual-stream dropout mask
 // 8-bit decisions (keep iff byte >= thr8, thr8 = round(256 p), scale 256 / (256 - thr8): the same
 // quantised p as the attention dropout).  Element (m, n) of a row-major [M, N] tensor takes byte
-// (n & 3) of word ((n >> 4) & 3) of Philox call ((m * ceil(N / 64) + (n >> 6)) * 4 + ((n >> 2) & 3)).
-// A GEMM epilogue lane holding C[m][n..n+3] for the four 16-column fragments of one 64-column block
-// (n = 64 b + 16 j + 4 g) therefore draws ONE call for its 16 elements (4x fewer than a call per 4),
-// while a thread owning 8 consecutive elements draws two.
+// (n & 3) of the word  fmix32(m * ceil(N / 4) + (n >> 2) + key(seed))  (32-bit index arithmetic:
+// exact below 2^32 words, i.e. 16 G elements per tensor).  One word per 4 consecutive elements:
+// a GEMM epilogue lane holding C[m][n..n+3] draws exactly one, a thread owning 8 consecutive
+// elements two.  The murmur3 finaliser is 2 multiplies per word; the Philox-4x32-10 call this
+// replaced cost 40 quarter-rate multiplies per 16 decisions and made the standalone dropout-
+// backward kernels RNG-bound (each of their threads used one word of two calls).
 constexpr uint32_t kRowDropSalt = 0x0d0f0d0fu;
 
 inline uint32_t dropout_threshold8(float p) {
@@ -154,14 +156,23 @@ inline uint32_t dropout_threshold8(float p) {
 }
 inline float dropout_scale8(uint32_t thr8) { return thr8 >= 256 ? 0.f : 256.f / (float)(256 - thr8); }
 
-MG_DEVICE uint4 rowdrop_call(uint64_t seed, long m, int n, int N) {
-  const uint64_t c = ((uint64_t)m * (uint64_t)((N + 63) >> 6) + (uint64_t)(n >> 6)) * 4u + ((n >> 2) & 3);
-  return philox4x32(make_uint4((uint32_t)c, (uint32_t)(c >> 32), kRowDropSalt, 0u),
-                    make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+MG_DEVICE uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
 }
 
-MG_DEVICE uint32_t word_of(const uint4& r, int w) {
-  return w == 0 ? r.x : (w == 1 ? r.y : (w == 2 ? r.z : r.w));
+// per-seed key (wave-uniform: scalar work)
+MG_DEVICE uint32_t rowdrop_key(uint64_t seed) {
+  return fmix32((uint32_t)seed ^ kRowDropSalt) ^ ((uint32_t)(seed >> 32) * 0x9E3779B1u);
+}
+
+// decision word of elements (m, n..n+3), n % 4 == 0
+MG_DEVICE uint32_t rowdrop_word(uint32_t key, long m, int n, int N) {
+  return fmix32((uint32_t)m * (uint32_t)((N + 3) >> 2) + (uint32_t)(n >> 2) + key);
 }
 
 // apply the mask to 4 consecutive elements whose 4 decision bytes are `word`
@@ -172,9 +183,9 @@ MG_DEVICE void rowdrop4(float* v, uint32_t word, uint32_t thr8, float scale) {
 
 // 8 consecutive elements (m, n..n+7), n % 8 == 0
 MG_DEVICE void rowdrop8(float (&v)[8], uint64_t seed, long m, int n, int N, uint32_t thr8, float scale) {
-  const int w = (n >> 4) & 3;
-  rowdrop4(v, word_of(rowdrop_call(seed, m, n, N), w), thr8, scale);
-  rowdrop4(v + 4, word_of(rowdrop_call(seed, m, n + 4, N), w), thr8, scale);
+  const uint32_t key = rowdrop_key(seed);
+  rowdrop4(v, rowdrop_word(key, m, n, N), thr8, scale);
+  rowdrop4(v + 4, rowdrop_word(key, m, n + 4, N), thr8, scale);
 }
 
 // ---------------------------------------------------------------- GELU (tanh approximation)

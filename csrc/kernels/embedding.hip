@@ -33,7 +33,7 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict_
     unpack8(ld16(wpe + (long)t * D + c), p);
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[j] += p[j];
-    if (use_dropout) dropout8(a, seed, (uint64_t)m * D + c, thr, scale);
+    if (use_dropout) rowdrop8(a, seed, m, c, D, thr, scale);
     st16(out + m * D + c, pack8(a));
   }
 }
@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256) void emb_bwd_wte_kernel(const int64_t* __restr
     float g[8];
     if (c < D) {
       unpack8(ld16(dout + m * D + c), g);
-      if (use_dropout) dropout8(g, seed, (uint64_t)m * D + c, thr, scale);
+      if (use_dropout) rowdrop8(g, seed, m, c, D, thr, scale);
     }
     // transpose through lanes so each atomic wave-instruction touches 64 consecutive floats:
     // element j of lane L is column c0 + 8L + j. Atomic k handles columns c0 + 64k + lane,
@@ -88,7 +88,7 @@ __global__ __launch_bounds__(64) void emb_bwd_wpe_kernel(const bf16_t* __restric
     const long m = (long)b * T + t;
     float g[8];
     unpack8(ld16(dout + m * D + c), g);
-    if (use_dropout) dropout8(g, seed, (uint64_t)m * D + c, thr, scale);
+    if (use_dropout) rowdrop8(g, seed, m, c, D, thr, scale);
 #pragma unroll
     for (int j = 0; j < 8; ++j) s[j] += g[j];
   }
@@ -103,16 +103,16 @@ namespace mg {
 
 void embedding_fwd(const int64_t* idx, const bf16_t* wte, const bf16_t* wpe, bf16_t* out, int M,
                    int T, int D, float p, uint64_t seed, hipStream_t stream) {
-  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  emb_fwd_kernel<<<cdiv(M, 4), 256, 0, stream>>>(idx, wte, wpe, out, M, T, D, seed,
-                                                 dropout_threshold(p), scale, p > 0.f,
+  const uint32_t thr = dropout_threshold8(p);  // the 8-bit residual-stream mask (common.h)
+  emb_fwd_kernel<<<cdiv(M, 4), 256, 0, stream>>>(idx, wte, wpe, out, M, T, D, seed, thr,
+                                                 dropout_scale8(thr), p > 0.f,
                                                  graph_seed_ofs());
 }
 
 void embedding_bwd(const int64_t* idx, const bf16_t* dout, float* dwte, float* dwpe, int M, int T,
                    int D, float p, uint64_t seed, hipStream_t stream) {
-  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  const uint32_t thr = dropout_threshold(p);
+  const uint32_t thr = dropout_threshold8(p);
+  const float scale = dropout_scale8(thr);
   if (dwte)
     emb_bwd_wte_kernel<<<cdiv(M, 4), 256, 0, stream>>>(idx, dout, dwte, M, D, seed, thr, scale,
                                                        p > 0.f, graph_seed_ofs());

@@ -307,6 +307,7 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
       if (args.bias && nb + j * 16 < nlim) bs[j] = *reinterpret_cast<const uint2*>(args.bias + nb + j * 16);
   }
   const bf16_t* __restrict__ side = EPI == 3 ? args.resid : args.aux;
+  const uint32_t dkey = EPI == 3 ? rowdrop_key(eff_seed(args.seed, args.sofs)) : 0u;  // dropout key
   const bool full = nw + CF::WTN <= nlim && mw + CF::WTM <= args.M;  // wave-uniform: no per-piece checks
 #pragma unroll
   for (int c = 0; c < CF::FM / CHF; ++c) {
@@ -327,7 +328,6 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
       const int i = c * CHF + ii;
       const int m = mw + i * 16 + (lane & 15);
       char* row = st + (ii * 16 + (lane & 15)) * S;
-      uint4 rnd = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
       for (int j = 0; j < CF::FN; ++j) {
         const int n = nb + j * 16;
@@ -346,11 +346,7 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
               make_uint2(pack2(g0.x, g0.y), pack2(g1.x, g1.y));
         }
         if constexpr (EPI == 3) {
-          if (args.thr) {  // one Philox call per 64-column block of this lane's row (common.h rowdrop)
-            const int w16 = (n >> 4) & 3;
-            if (CF::WTN % 64 == 0 ? (j & 3) == 0 : (j == 0 || w16 == 0)) rnd = rowdrop_call(eff_seed(args.seed, args.sofs), m, n, args.N);
-            rowdrop4(v, word_of(rnd, CF::WTN % 64 == 0 ? (j & 3) : w16), args.thr, args.scale);
-          }
+          if (args.thr) rowdrop4(v, rowdrop_word(dkey, m, n, args.N), args.thr, args.scale);  // common.h
         }
         if constexpr (F32)
           *reinterpret_cast<float4*>(row + col * 4) = make_float4(v[0], v[1], v[2], v[3]);
@@ -411,6 +407,7 @@ MG_DEVICE void epilogue(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int 
   const int nlim = (EPI == 0 && !OUTF32) ? (int)args.ldc : args.N;
   const int nb = n0 + wn * CF::WTN + (lane >> 4) * 4;
   const bf16_t* __restrict__ bias = args.bias;
+  const uint32_t dkey = EPI == 3 ? rowdrop_key(eff_seed(args.seed, args.sofs)) : 0u;  // dropout key
   uint2 bs[CF::FN];
   float csum[EPI == 4 ? CF::FN : 1][4];  // EPI 4 bias gradient: this lane's column partial sums
 #pragma unroll
@@ -442,7 +439,6 @@ MG_DEVICE void epilogue(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int 
         side[j] = *reinterpret_cast<const uint2*>(args.aux + rowoff + n);
       }
     }
-    uint4 rnd = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
     for (int j = 0; j < CF::FN; ++j) {
       const int n = nb + j * 16;
@@ -469,12 +465,7 @@ MG_DEVICE void epilogue(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int 
           *reinterpret_cast<uint2*>(args.aux + off) = make_uint2(pack2(gd[0], gd[1]), pack2(gd[2], gd[3]));
         }
         if constexpr (EPI == 3) {
-          if (args.thr) {  // one Philox call per 64-column block of this lane's row (common.h rowdrop)
-            // (wave tiles 64 / 128 wide start on a 64-column block; the 96-wide W4 tile may not)
-            const int w16 = (n >> 4) & 3;
-            if (CF::WTN % 64 == 0 ? (j & 3) == 0 : (j == 0 || w16 == 0)) rnd = rowdrop_call(eff_seed(args.seed, args.sofs), m, n, args.N);
-            rowdrop4(v, word_of(rnd, CF::WTN % 64 == 0 ? (j & 3) : w16), args.thr, args.scale);
-          }
+          if (args.thr) rowdrop4(v, rowdrop_word(dkey, m, n, args.N), args.thr, args.scale);  // common.h
           v[0] += bf2f(side[j].x & 0xffffu); v[1] += bf2f(side[j].x >> 16);
           v[2] += bf2f(side[j].y & 0xffffu); v[3] += bf2f(side[j].y >> 16);
         }
