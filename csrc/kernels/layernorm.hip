@@ -227,7 +227,28 @@ __global__ __launch_bounds__(256) void ln_colsum_kernel(const float* __restrict_
 namespace mg {
 
 // >= 32 rows per block (4 waves x 2 rows x >= 4 iterations) up to 1024 blocks
-int ln_bwd_grid(int M) { return M / 32 < 1 ? 1 : (M / 32 > 1024 ? 1024 : M / 32); }
+// One resident wave of blocks: the kernel grid-strides over rows, and a grid of more blocks than
+// fit the CUs at once (1024 at D = 768, where 150 VGPRs leave room for 3 blocks per CU = 768)
+// ran a second, one-third-full round.  Occupancy from the runtime for the instantiation D selects.
+template <int NV>
+static int ln_bwd_resident() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)ln_bwd_kernel<NV>, 256,
+                                                       sizeof(float) * 8 * NV * 512);
+    n = std::max(1, cus * std::max(1, per_cu));
+  }
+  return n;
+}
+
+int ln_bwd_grid(int M, int D) {
+  const int cap = D <= 512 ? ln_bwd_resident<1>() : D <= 1024 ? ln_bwd_resident<2>()
+                  : D <= 2048 ? ln_bwd_resident<4>() : ln_bwd_resident<8>();
+  return std::max(1, std::min(M / 32, cap));
+}
 
 #define MG_LN_DISPATCH(KERNEL, ...)                                                   \
   do {                                                                                \
@@ -247,13 +268,13 @@ void layernorm_fwd(const bf16_t* x, const bf16_t* w, const bf16_t* b, bf16_t* y,
 void layernorm_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const float* mean,
                    const float* rstd, const bf16_t* dres, bf16_t* dx, float* dw, float* db,
                    float* workspace, int M, int D, hipStream_t stream) {
-  const int grid = ln_bwd_grid(M);
+  const int grid = ln_bwd_grid(M, D);
   const size_t smem = sizeof(float) * 8 * D;
   MG_LN_DISPATCH(ln_bwd_kernel, dy, x, w, mean, rstd, dres, dx, workspace, M, D);
   ln_colsum_kernel<<<dim3(cdiv(2 * D, 64), cdiv(grid, 32)), 256, 0, stream>>>(workspace, grid, D, dw, db);
 }
 
 // floats of partial [dgamma | dbeta] rows layernorm_bwd needs
-size_t layernorm_bwd_workspace(int M, int D) { return (size_t)ln_bwd_grid(M) * 2 * D; }
+size_t layernorm_bwd_workspace(int M, int D) { return (size_t)ln_bwd_grid(M, D) * 2 * D; }
 
 }  // namespace mg
