@@ -45,9 +45,21 @@ _WGRAD_BLAS = os.environ.get("MINGPT_WGRAD_BLAS", "0") == "1"
 _QKV_BLAS = os.environ.get("MINGPT_QKV_BLAS", "1") == "1"
 
 
+# Library calls cost more host time per launch than the extension's; small models (gpt-mini:
+# M = 8192, K = 192) are launch-bound and ran 15 % slower through hipBLASLt (one-box A/B), so
+# only GEMMs of at least this many multiply-adds take the library path.
+_BLAS_MIN_MNK = 5e9
+
+
+def _big(m, n, k):
+    return float(m) * n * k >= _BLAS_MIN_MNK
+
+
 def _dgrad(dy, w):
     """dX = dY @ W for a plain (epilogue-free) data gradient."""
-    return torch.mm(dy, w) if _DGRAD_BLAS else G.gemm_dgrad(dy, w)
+    if _DGRAD_BLAS and _big(dy.shape[0], w.shape[1], w.shape[0]):
+        return torch.mm(dy, w)
+    return G.gemm_dgrad(dy, w)
 
 
 def _wgrad(dy, x, main_grad):
@@ -91,7 +103,10 @@ class TransformerBlockFn(torch.autograd.Function):
         seeds = (new_seed() if p_attn > 0 else 0, new_seed() if p_resid > 0 else 0,
                  new_seed() if p_resid > 0 else 0)
         h, mean1, rstd1 = C.layernorm_fwd(x, ln1w, ln1b, eps)
-        qkv = torch.addmm(bqkv, h, wqkv.t()) if _QKV_BLAS else G.gemm_nt(h, wqkv, bias=bqkv, epi="bias")
+        if _QKV_BLAS and _big(h.shape[0], wqkv.shape[0], h.shape[1]):
+            qkv = torch.addmm(bqkv, h, wqkv.t())
+        else:
+            qkv = G.gemm_nt(h, wqkv, bias=bqkv, epi="bias")
         y, lse, amask = C.attention_fwd(qkv, B, T, H, float(p_attn), seeds[0])
         x1 = G.gemm_nt(y, wo, bias=bo, epi="resid", resid=x, p=p_resid, seed=seeds[1])
         h2, mean2, rstd2 = C.layernorm_fwd(x1, ln2w, ln2b, eps)
@@ -173,7 +188,7 @@ class HeadLossFn(torch.autograd.Function):
         ld = (V + 127) // 128 * 128
         h, mean, rstd = C.layernorm_fwd(x, lnw, lnb, eps)
         ctx.wpad = None
-        if _LMHEAD_BLAS:
+        if _LMHEAD_BLAS and _big(h.shape[0], ld, h.shape[1]):
             ctx.wpad = _padded_weight(w, ld)
             logits = torch.mm(h, ctx.wpad.t())
         else:
