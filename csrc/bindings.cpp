@@ -127,6 +127,30 @@ at::Tensor xent_bwd(const at::Tensor& logits, const at::Tensor& targets, const a
   return dl;
 }
 
+// one-pass training cross-entropy: returns (out[2] = {loss, 1/n_valid}, dlogits = (softmax -
+// onehot) / n_valid); empty list when the row width is outside the fused kernel's range
+std::vector<at::Tensor> xent_fused(const at::Tensor& logits, const at::Tensor& targets, int64_t V) {
+  CHECK_BF16(logits); CHECK_I64(targets); CHECK_CONTIG(logits); CHECK_CONTIG(targets);
+  const int64_t ld = logits.size(-1), M = logits.numel() / ld;
+  TORCH_CHECK(targets.numel() == M && V <= ld && ld % 8 == 0, "xent_fused: shape mismatch");
+  if (mg::xent_fused_nv((int)ld) == 0) return {};
+  DevGuard g(logits.device());
+  auto opts = logits.options().dtype(at::kFloat);
+  auto loss_row = at::empty({M}, opts);
+  auto out = at::empty({2}, opts);
+  auto dl = at::empty_like(logits);
+  mg::xent_fused(bp(logits), targets.data_ptr<int64_t>(), fp(loss_row), fp(out), bp(dl), (int)M,
+                 (int)V, (int)ld, cur_stream());
+  return {out, dl};
+}
+
+void xent_scale_(const at::Tensor& dlogits, const at::Tensor& gscale) {
+  CHECK_BF16(dlogits); CHECK_CONTIG(dlogits); CHECK_F32(gscale);
+  TORCH_CHECK(dlogits.numel() % 8 == 0, "xent_scale_: numel must be a multiple of 8");
+  DevGuard g(dlogits.device());
+  mg::xent_scale(bp(dlogits), fp(gscale), dlogits.numel(), cur_stream());
+}
+
 // ------------------------------------------------------------------------------- hipGraph mode
 // While set, launches read dropout-seed offsets from seed_ofs[0] (uint64, bumped inside the graph
 // each replay) and AdamW reads {lr, step} from opt_hp (fp32[2], written before each replay).
@@ -421,6 +445,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embedding_bwd", &embedding_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
+  m.def("xent_fused", &xent_fused);
+  m.def("xent_scale_", &xent_scale_);
   m.def("set_graph_state", &set_graph_state, py::arg("seed_ofs") = py::none(), py::arg("opt_hp") = py::none());
   m.def("grad_sumsq", &grad_sumsq);
   m.def("adamw_step", &adamw_step);

@@ -28,6 +28,10 @@ void xent_fwd(const bf16_t* logits, const int64_t* targets, float* loss_row, flo
               int M, int V, int ld, hipStream_t stream);
 void xent_bwd(const bf16_t* logits, const int64_t* targets, const float* lse, const float* gscale,
               const float* inv_n, bf16_t* dlogits, int M, int V, int ld, hipStream_t stream);
+int xent_fused_nv(int ld);
+void xent_fused(const bf16_t* logits, const int64_t* targets, float* loss_row, float* out,
+                bf16_t* dlogits, int M, int V, int ld, hipStream_t stream);
+void xent_scale(bf16_t* dlogits, const float* gscale, long n, hipStream_t stream);
 
 // adamw.hip (also holds the hipGraph-mode device state; see common.h eff_seed)
 void set_graph_state(const uint64_t* seed_ofs, const float* opt_hp);

@@ -166,6 +166,10 @@ class TransformerBlockFn(torch.autograd.Function):
 # PERF.md).  The weight gradient (fp32 accumulate into main_grad) and every fused GEMM stay on the
 # HIP kernels.  MINGPT_LMHEAD_BLAS=0 routes the head through gemm.hip as well.
 _LMHEAD_BLAS = os.environ.get("MINGPT_LMHEAD_BLAS", "1") == "1"
+# Training cross-entropy in one pass over the logits (xent.hip xent_fused: loss and
+# dlogits = (softmax - onehot) / n_valid written in forward, grad_out applied in backward).
+# MINGPT_XENT_FUSED=0 keeps the two-pass fwd / bwd kernels.
+_XENT_FUSED = os.environ.get("MINGPT_XENT_FUSED", "1") == "1"
 
 
 def _padded_weight(w, ld):
@@ -193,8 +197,14 @@ class HeadLossFn(torch.autograd.Function):
             logits = torch.mm(h, ctx.wpad.t())
         else:
             logits = G.gemm_nt(h, w, ld=ld)
-        out, lse = C.xent_fwd(logits, targets, V)
-        ctx.save_for_backward(x, h, mean, rstd, logits, targets, lse, out)
+        fused = C.xent_fused(logits, targets, V) if _XENT_FUSED and any(ctx.needs_input_grad) else []
+        if fused:  # the backward never reads the logits again
+            out, dlogits = fused
+            ctx.save_for_backward(x, h, mean, rstd, dlogits, None, None, out)
+        else:
+            out, lse = C.xent_fwd(logits, targets, V)
+            ctx.save_for_backward(x, h, mean, rstd, logits, targets, lse, out)
+        ctx.fused = bool(fused)
         ctx.params = (lnw, lnb, w)
         ctx.eps = eps
         for prm in ctx.params:
@@ -210,7 +220,11 @@ class HeadLossFn(torch.autograd.Function):
         lnw, lnb, w = ctx.params
         V = w.shape[0]
         gscale = dloss.reshape(1).float().contiguous()
-        dlogits = C.xent_bwd(logits, targets, lse, gscale, out, V)
+        if ctx.fused:
+            dlogits = logits
+            C.xent_scale_(dlogits, gscale)  # no-op on the device when grad_out == 1
+        else:
+            dlogits = C.xent_bwd(logits, targets, lse, gscale, out, V)
         del logits
         bw, mw = grad_target(w)
         G.gemm_tn_acc(dlogits, h, bw, n_valid=V)

@@ -93,6 +93,28 @@ def test_cross_entropy(M, V, ld):
     assert (dl[:, V:] == 0).all()
 
 
+@pytest.mark.parametrize("M,V,ld,gs", [(40, 50257, 50304, 1.0), (33, 50257, 50304, 0.5),
+                                       (9, 40000, 40064, 1.0), (5, 65536, 65536, 3.0)])
+def test_cross_entropy_fused(M, V, ld, gs):
+    """one-pass xent (loss + dlogits in forward, grad_out applied by xent_scale_) vs fp32 torch"""
+    C = ext()
+    logits = _bf(M, ld, scale=3.0, seed=9)
+    tgt = torch.randint(0, V, (M,), device=DEV)
+    tgt[::4] = -1
+    tgt[1] = V - 1
+    res = C.xent_fused(logits, tgt, V)
+    assert res, "fused cross-entropy must cover this row width"
+    out, dl = res
+    lr = logits.float()[:, :V].clone().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(lr, tgt, ignore_index=-1)
+    torch.testing.assert_close(out[0], ref.detach(), atol=1e-3, rtol=1e-3)
+    ref.backward(torch.tensor(gs, device=DEV))
+    C.xent_scale_(dl, torch.tensor([gs], device=DEV))
+    _close(dl[:, :V], lr.grad, atol=2e-3)
+    assert (dl[:, V:] == 0).all()
+    assert C.xent_fused(logits[:, :128].contiguous(), tgt, 100) == []  # outside the fused range
+
+
 def test_adamw_matches_torch():
     C = ext()
     sizes = [1000, 37, 4096, 5]
