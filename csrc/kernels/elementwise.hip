@@ -98,18 +98,20 @@ __global__ __launch_bounds__(256) void dropout_bwd_kernel(const bf16_t* __restri
 
 // Same row/column decomposition as bias_grad_kernel below, fused with the residual-dropout
 // backward: dx = dy * mask / (1-p) is written and its column sums are accumulated in one pass.
+template <int CVB>
 __global__ __launch_bounds__(256) void dropout_bias_grad_kernel(const bf16_t* __restrict__ dy,
                                                                 bf16_t* __restrict__ dx,
                                                                 float* __restrict__ db, int M, int N,
                                                                 uint64_t seed, uint32_t thr,
                                                                 float scale, const uint64_t* sofs) {
-  __shared__ __attribute__((aligned(16))) float red[4][512];
+  constexpr int RG = 256 / CVB;  // rows in flight per block
+  __shared__ __attribute__((aligned(16))) float red[RG][CVB * 8];
   seed = eff_seed(seed, sofs);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 512 + lane * 8;
+  const int cv = threadIdx.x % CVB, rg = threadIdx.x / CVB;
+  const int c = (blockIdx.x * CVB + cv) * 8;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (c < N) {
-    for (long r = (long)blockIdx.y * 4 + w; r < M; r += (long)gridDim.y * 4) {
+    for (long r = (long)blockIdx.y * RG + rg; r < M; r += (long)gridDim.y * RG) {
       float g[8];
       const long e = r * N + c;
       unpack8(ld16(dy + e), g);
@@ -120,25 +122,32 @@ __global__ __launch_bounds__(256) void dropout_bias_grad_kernel(const bf16_t* __
     }
   }
 #pragma unroll
-  for (int j = 0; j < 8; ++j) red[w][lane * 8 + j] = s[j];
+  for (int j = 0; j < 8; ++j) red[rg][cv * 8 + j] = s[j];
   __syncthreads();
-  for (int k = threadIdx.x; k < 512; k += 256) {
-    const int col = blockIdx.x * 512 + k;
-    if (col < N) atomicAdd(db + col, red[0][k] + red[1][k] + red[2][k] + red[3][k]);
+  for (int k = threadIdx.x; k < CVB * 8; k += 256) {
+    const int col = blockIdx.x * CVB * 8 + k;
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < RG; ++i) t += red[i][k];
+    if (col < N) atomicAdd(db + col, t);
   }
 }
 
-// grid = (ceil(N/512), RB); block = 256 (4 waves).  Wave w of block (cx, ry) sums rows
-// r = ry*4 + w, stepping by 4*RB, over columns cx*512 + lane*8 .. +8; LDS folds the 4 waves;
-// one fp32 atomic per column per block-row (RB-way, tiny).
+// grid = (ceil(N / (8 CVB)), RB); block = 256 threads = RG = 256 / CVB row groups of CVB lanes,
+// each lane owning 8 columns.  CVB = 32 when N / 8 is a multiple of 32 but not of 64 (N = 768:
+// three full blocks instead of two with a quarter of the lanes idle).  Row group g of block
+// (cx, ry) sums rows r = ry*RG + g, stepping by RG*RB; LDS folds the row groups; one fp32 atomic
+// per column per block-row (RB-way, tiny).
+template <int CVB>
 __global__ __launch_bounds__(256) void bias_grad_kernel(const bf16_t* __restrict__ dy,
                                                         float* __restrict__ db, int M, int N) {
-  __shared__ __attribute__((aligned(16))) float red[4][512];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 512 + lane * 8;
+  constexpr int RG = 256 / CVB;
+  __shared__ __attribute__((aligned(16))) float red[RG][CVB * 8];
+  const int cv = threadIdx.x % CVB, rg = threadIdx.x / CVB;
+  const int c = (blockIdx.x * CVB + cv) * 8;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (c < N) {
-    for (long r = (long)blockIdx.y * 4 + w; r < M; r += (long)gridDim.y * 4) {
+    for (long r = (long)blockIdx.y * RG + rg; r < M; r += (long)gridDim.y * RG) {
       float g[8];
       unpack8(ld16(dy + r * N + c), g);
 #pragma unroll
@@ -146,11 +155,14 @@ __global__ __launch_bounds__(256) void bias_grad_kernel(const bf16_t* __restrict
     }
   }
 #pragma unroll
-  for (int j = 0; j < 8; ++j) red[w][lane * 8 + j] = s[j];
+  for (int j = 0; j < 8; ++j) red[rg][cv * 8 + j] = s[j];
   __syncthreads();
-  for (int k = threadIdx.x; k < 512; k += 256) {
-    const int col = blockIdx.x * 512 + k;
-    if (col < N) atomicAdd(db + col, red[0][k] + red[1][k] + red[2][k] + red[3][k]);
+  for (int k = threadIdx.x; k < CVB * 8; k += 256) {
+    const int col = blockIdx.x * CVB * 8 + k;
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < RG; ++i) t += red[i][k];
+    if (col < N) atomicAdd(db + col, t);
   }
 }
 
@@ -242,14 +254,27 @@ void dropout_bwd(const bf16_t* dy, bf16_t* dx, long M, int N, float p, uint64_t 
                                                        graph_seed_ofs());
 }
 
+// lanes per row chunk: 32 when it fills every lane and 64 would not
+static int bias_cvb(int N) { return ((N / 8) % 64 != 0 && (N / 8) % 32 == 0) ? 32 : 64; }
+
+static dim3 bias_grid(long M, int N, int cvb) {
+  const int cx = cdiv(N, cvb * 8);
+  int ry = (int)std::max<long>(1, std::min<long>(512, M / 64));  // >= 64 rows per block: few atomics
+  while (cx * ry > 2048 && ry > 1) ry >>= 1;  // ~2048 blocks: every CU busy, few atomics per column
+  return dim3(cx, ry);
+}
+
 void dropout_bias_grad(const bf16_t* dy, bf16_t* dx, float* db, long M, int N, float p, uint64_t seed,
                        hipStream_t stream) {
-  const int cx = cdiv(N, 512);
-  int ry = (int)std::max<long>(1, std::min<long>(512, M / 64));  // >= 64 rows per block: few atomics
-  while (cx * ry > 2048 && ry > 1) ry >>= 1;
   const uint32_t thr = dropout_threshold8(p);
-  dropout_bias_grad_kernel<<<dim3(cx, ry), 256, 0, stream>>>(dy, dx, db, (int)M, N, seed, thr,
-                                                             dropout_scale8(thr), graph_seed_ofs());
+  const int cvb = bias_cvb(N);
+  const dim3 grid = bias_grid(M, N, cvb);
+  if (cvb == 32)
+    dropout_bias_grad_kernel<32><<<grid, 256, 0, stream>>>(dy, dx, db, (int)M, N, seed, thr,
+                                                           dropout_scale8(thr), graph_seed_ofs());
+  else
+    dropout_bias_grad_kernel<64><<<grid, 256, 0, stream>>>(dy, dx, db, (int)M, N, seed, thr,
+                                                           dropout_scale8(thr), graph_seed_ofs());
 }
 
 void transpose(const bf16_t* src, bf16_t* dst, int R, int C, int ldd, hipStream_t stream) {
@@ -257,10 +282,12 @@ void transpose(const bf16_t* src, bf16_t* dst, int R, int C, int ldd, hipStream_
 }
 
 void bias_grad(const bf16_t* dy, float* db, long M, int N, hipStream_t stream) {
-  const int cx = cdiv(N, 512);
-  int ry = (int)std::max<long>(1, std::min<long>(512, M / 64));  // >= 64 rows per block: few atomics
-  while (cx * ry > 2048 && ry > 1) ry >>= 1;  // ~2048 blocks: every CU busy, few atomics per column
-  bias_grad_kernel<<<dim3(cx, ry), 256, 0, stream>>>(dy, db, (int)M, N);
+  const int cvb = bias_cvb(N);
+  const dim3 grid = bias_grid(M, N, cvb);
+  if (cvb == 32)
+    bias_grad_kernel<32><<<grid, 256, 0, stream>>>(dy, db, (int)M, N);
+  else
+    bias_grad_kernel<64><<<grid, 256, 0, stream>>>(dy, db, (int)M, N);
 }
 
 }  // namespace mg

@@ -155,9 +155,10 @@ def test_adamw_matches_torch():
     _close(param, master, atol=1e-2)
 
 
-def test_elementwise():
+@pytest.mark.parametrize("N", [768, 2304, 3072, 520])  # 32- and 64-lane bias-grad row chunks
+def test_elementwise(N):
     C = ext()
-    M, N = 130, 768
+    M = 130
     x, b, r = _bf(M, N, seed=9), _bf(N, seed=10), _bf(M, N, seed=11)
     pre = torch.empty_like(x)
     y = C.bias_act(x, b, pre, 1)
