@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--vocab", type=int, default=50257, help="65 = chargpt's character vocabulary")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--zero1", action="store_true",
+                    help="shard the AdamW state over the ranks (reduce-scatter + all-gather)")
     ap.add_argument("--profile", default="", help="write a torch.profiler trace to this dir")
     ap.add_argument("--graph", action="store_true",
                     help="replay each step as one hipGraph (single GPU; StepEngine.graph_step)")
@@ -64,7 +66,7 @@ def main():
     torch.manual_seed(1234)  # identical init on every rank (the engine also broadcasts rank 0)
     model = GPT(cfg, verbose=info.rank == 0)
     eng = StepEngine(model, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, grad_clip=1.0,
-                     bucket_mb=a.bucket_mb)
+                     bucket_mb=a.bucket_mb, zero1=a.zero1)
     g = torch.Generator(device=eng.device).manual_seed(99 + info.rank)
     nb = 4
     xs = [torch.randint(0, a.vocab, (a.batch, a.seq), device=eng.device, generator=g) for _ in range(nb)]
@@ -114,7 +116,7 @@ def main():
             "dtype": "bf16",
             "data": "synthetic (random tokens, random-init weights)",
             "config": {"model": a.model, "global_batch": a.batch * N, "seq_len": a.seq,
-                       "parallelism": f"dp{N}", "micro_batch_per_gpu": a.batch, "dropout": a.dropout,
+                       "parallelism": f"dp{N}" + ("-zero1" if eng.zero1 else ""), "micro_batch_per_gpu": a.batch, "dropout": a.dropout,
                        "bucket_mb": a.bucket_mb, "hip_graph": bool(a.graph and N == 1)},
             "loss": round(loss_v, 4),
             "max_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2),

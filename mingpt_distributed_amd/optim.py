@@ -71,7 +71,7 @@ class FlatParamStore:
     """All parameters of ``model`` as views into flat buffers (see module docstring)."""
 
     def __init__(self, model: nn.Module, compute_dtype: Optional[torch.dtype] = None,
-                 device: Optional[torch.device] = None):
+                 device: Optional[torch.device] = None, pad_multiple: int = ALIGN):
         named = list(model.named_parameters())  # dedups tied weights
         if device is None:
             device = named[0][1].device
@@ -90,7 +90,8 @@ class FlatParamStore:
             self.offsets.append(off)
             self.numels.append(p.numel())
             off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
-        self.total = off
+        # ZeRO-1 pads the tail so the buffer splits into equal, 64-element aligned rank shards
+        self.total = (off + pad_multiple - 1) // pad_multiple * pad_multiple
         f32 = dict(dtype=torch.float32, device=device)
         self.master = torch.zeros(self.total, **f32)
         self.grad = torch.zeros(self.total, **f32)

@@ -49,7 +49,8 @@ def _fold_grad(p):
 class StepEngine:
     def __init__(self, model: torch.nn.Module, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
                  weight_decay: float = 0.1, grad_clip: float = 1.0, decay_names=None,
-                 device: Optional[torch.device] = None, bucket_mb: float = 32.0, reduce_dtype=None):
+                 device: Optional[torch.device] = None, bucket_mb: float = 32.0, reduce_dtype=None,
+                 zero1: bool = False):
         if device is None:
             info = D.info()
             if info.device.type == "cuda":
@@ -62,11 +63,22 @@ class StepEngine:
         self.model = model.to(self.device)
         if decay_names is None:
             decay_names, _ = param_groups(model)
-        self.store = FlatParamStore(model, device=self.device)
-        self.opt = FusedAdamW(self.store, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
-                              decay_names=decay_names, grad_clip=grad_clip or 0.0)
-        self.dp = DataParallelEngine(self.store, bucket_mb=bucket_mb, reduce_dtype=reduce_dtype) \
-            if D.is_initialized() and torch.distributed.get_world_size() > 1 else None
+        multi = D.is_initialized() and torch.distributed.get_world_size() > 1
+        self.zero1 = bool(zero1 and multi)
+        okw = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, decay_names=decay_names,
+                   grad_clip=grad_clip or 0.0)
+        if self.zero1:  # optimizer state sharded over the ranks (parallel/zero.py)
+            from .parallel.zero import ZeroAdamW, ZeroGradEngine
+
+            self.store = FlatParamStore(model, device=self.device,
+                                        pad_multiple=64 * torch.distributed.get_world_size())
+            self.dp = ZeroGradEngine(self.store)
+            self.opt = ZeroAdamW(self.store, self.dp, **okw)
+        else:
+            self.store = FlatParamStore(model, device=self.device)
+            self.opt = FusedAdamW(self.store, **okw)
+            self.dp = DataParallelEngine(self.store, bucket_mb=bucket_mb, reduce_dtype=reduce_dtype) \
+                if multi else None
         self.world = self.dp.world if self.dp else 1
         self._hooks = []
         self.annotate = False  # record_function ranges (fwd/bwd/allreduce/optim) while profiling
@@ -234,6 +246,7 @@ class GPTTrainerConfig:
     max_steps_per_epoch: Optional[int] = None
     seed: int = 0
     save_every_steps: Optional[int] = None      # step-granular snapshots (mid-epoch resume)
+    zero1: bool = False                         # shard AdamW state over the ranks (parallel/zero.py)
     fault_inject_step: Optional[int] = None     # test hook: fail after this global step
     fault_inject_rank: Optional[int] = None     # ... on this rank only (None = every rank)
     fault_inject_mode: str = "raise"            # "raise" (InjectedFault) or "exit" (os._exit(13))
@@ -294,9 +307,9 @@ class GPTTrainer:
             self.config.snapshot_path = "gpt_snapshot.pt"
         clip = config.grad_norm_clip or 0.0
         if isinstance(optimizer, torch.optim.Optimizer):
-            self.engine = StepEngine.from_torch_optimizer(model, optimizer, clip)
+            self.engine = StepEngine.from_torch_optimizer(model, optimizer, clip, zero1=config.zero1)
         else:
-            self.engine = StepEngine(model, grad_clip=clip)
+            self.engine = StepEngine(model, grad_clip=clip, zero1=config.zero1)
         self.model = self.engine.model
         self.optimizer = self.engine.opt
         self.save_every = config.save_every or 1
@@ -339,6 +352,11 @@ class GPTTrainer:
 
             client = boto3.client("s3")
         client.upload_fileobj(buffer, u.netloc, u.path.lstrip("/"))
+
+    def _consolidate(self) -> None:
+        # ZeRO-1: masters and moments are sharded; gather them on every rank before rank 0 saves
+        if hasattr(self.engine.opt, "consolidate"):
+            self.engine.opt.consolidate()
 
     def _save_snapshot(self, epoch: int, epoch_step: int = 0) -> None:
         # every rank must take part in nothing here: called on global rank 0 only (D19)
@@ -458,8 +476,10 @@ class GPTTrainer:
             nlog += 1
             if train:
                 self.step += 1
-                if c.save_every_steps and self.step % c.save_every_steps == 0 and self.global_rank == 0:
-                    self._save_snapshot(epoch, epoch_step=idx + 1)
+                if c.save_every_steps and self.step % c.save_every_steps == 0:
+                    self._consolidate()
+                    if self.global_rank == 0:
+                        self._save_snapshot(epoch, epoch_step=idx + 1)
                 self._maybe_inject_fault()
             if idx % c.log_every == 0:
                 lg = D.all_reduce_mean(loss.float()).item()   # syncs the device: timing is honest
@@ -493,8 +513,10 @@ class GPTTrainer:
             for epoch in range(start, self.config.max_epochs):
                 tr = self._run_epoch(epoch, self.train_loader, True)
                 rec = {"epoch": epoch, "train_loss": tr}
-                if self.global_rank == 0 and epoch % self.save_every == 0:
-                    self._save_snapshot(epoch)
+                if epoch % self.save_every == 0:
+                    self._consolidate()
+                    if self.global_rank == 0:
+                        self._save_snapshot(epoch)
                 if self.test_loader is not None:
                     rec["test_loss"] = self._run_epoch(epoch, self.test_loader, False)
                 self.history.append(rec)
