@@ -54,8 +54,16 @@ def _run(cmd):
     return r
 
 
-def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+DEBUG_SO = os.path.join(ROOT, "build", "debug", "_C.so")
+
+
+def build(force: bool = False, jobs: int = 8, verbose: bool = True, debug: bool = False) -> str:
+    """Release: ``mingpt_distributed_amd/_C.so``.  ``debug=True``: the same sources with
+    ``-DMG_DEBUG`` (device-side range checks on token ids / targets, common.h MG_CHECK_INDEX) into
+    ``build/debug/_C.so``; load it with ``MINGPT_EXT_SO=build/debug/_C.so MINGPT_DEBUG_CHECKS=1``."""
+    flags = COMMON_FLAGS + (["-DMG_DEBUG"] if debug else [])
+    bdir = BUILD + "_debug" if debug else BUILD
+    os.makedirs(bdir, exist_ok=True)
     headers = glob.glob(os.path.join(ROOT, "csrc", "include", "*.h"))
     kernels = sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip")))
     incs, tlib, abi = _torch_paths()
@@ -64,15 +72,15 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
     jobs_list = []
     objs = []
     for src in kernels:
-        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        obj = os.path.join(bdir, os.path.basename(src) + ".o")
         objs.append(obj)
         if force or _newer(obj, [src] + headers):
-            jobs_list.append([HIPCC, *COMMON_FLAGS, "-x", "hip", "-c", "-o", obj, src])
+            jobs_list.append([HIPCC, *flags, "-x", "hip", "-c", "-o", obj, src])
     bsrc = os.path.join(ROOT, "csrc", "bindings.cpp")
-    bobj = os.path.join(BUILD, "bindings.o")
+    bobj = os.path.join(bdir, "bindings.o")
     objs.append(bobj)
     if force or _newer(bobj, [bsrc] + headers):
-        jobs_list.append([HIPCC, *COMMON_FLAGS, "-x", "hip", "-c", "-o", bobj,
+        jobs_list.append([HIPCC, *flags, "-x", "hip", "-c", "-o", bobj,
                           *["-I" + p for p in incs], "-I" + py_inc,
                           f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_C",
                           "-DTORCH_API_INCLUDE_EXTENSION_H", "-D__HIP_PLATFORM_AMD__=1",
@@ -84,7 +92,8 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
                 f.result()
                 if verbose:
                     print(f"[build_ext] compiled {os.path.relpath(futs[f], ROOT)}", flush=True)
-    out = os.path.join(PKG, "_C.so")
+    out = DEBUG_SO if debug else os.path.join(PKG, "_C.so")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     if force or _newer(out, objs):
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out, *objs,
               "-L" + tlib, "-Wl,-rpath," + tlib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
@@ -115,7 +124,10 @@ if __name__ == "__main__":
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 8))
     ap.add_argument("--tools", action="store_true", help="also build tools/*.cpp executables")
+    ap.add_argument("--debug", action="store_true", help="also build the MG_DEBUG variant")
     a = ap.parse_args()
     build(force=a.force, jobs=a.jobs)
+    if a.debug:
+        build(force=a.force, jobs=a.jobs, debug=True)
     if a.tools:
         build_tools()

@@ -82,7 +82,7 @@ at::Tensor embedding_fwd(const at::Tensor& idx, const at::Tensor& wte, const at:
   DevGuard g(idx.device());
   auto out = at::empty({B, T, D}, wte.options());
   mg::embedding_fwd(idx.data_ptr<int64_t>(), bp(wte), bp(wpe), bp(out), (int)(B * T), (int)T,
-                    (int)D, (float)p, (uint64_t)seed, cur_stream());
+                    (int)D, (int)wte.size(0), (float)p, (uint64_t)seed, cur_stream());
   return out;
 }
 
@@ -96,7 +96,7 @@ void embedding_bwd(const at::Tensor& idx, const at::Tensor& dout,
   if (dwpe.has_value()) { CHECK_F32(*dwpe); TORCH_CHECK(dwpe->size(-1) == D && dwpe->size(0) >= T); }
   DevGuard g(idx.device());
   mg::embedding_bwd(idx.data_ptr<int64_t>(), bp(dout), fp_opt(dwte), fp_opt(dwpe), (int)(B * T),
-                    (int)T, (int)D, (float)p, (uint64_t)seed, cur_stream());
+                    (int)T, (int)D, dwte.has_value() ? (int)(dwte->numel() / D) : 0, (float)p, (uint64_t)seed, cur_stream());
 }
 
 // ------------------------------------------------------------------------------- cross entropy
@@ -442,6 +442,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("embedding_fwd", &embedding_fwd);
+  // debug builds: OR of the device error words (1/2 = token id out of range in embedding fwd/bwd,
+  // 4 = cross-entropy target >= V), cleared on read; always 0 in release builds
+  m.def("debug_error_bits", []() -> int64_t { return (int64_t)mg::debug_error_bits(); });
+  m.def("debug_build", []() {
+#ifdef MG_DEBUG
+    return true;
+#else
+    return false;
+#endif
+  });
   m.def("embedding_bwd", &embedding_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);

@@ -228,3 +228,22 @@ MG_DEVICE void gelu2(f32x2 x, f32x2& y, f32x2& g) {
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace mg
+
+// Debug builds (build_ext.py --debug => -DMG_DEBUG, loaded with MINGPT_EXT_SO): data-dependent
+// indices (token ids, targets) are range-checked on the device.  A bad index is clamped to a safe
+// value (no out-of-bounds access, no GPU fault) and recorded with a vector atomic in a device
+// error word (hipMalloc'd, mg::debug_err_word(); nullptr in release builds, where the check
+// compiles away).  The host reads and clears it after each op (mg::debug_error_bits,
+// ops/_ext.py MINGPT_DEBUG_CHECKS=1) and raises naming the op.
+namespace mg {
+unsigned int* debug_err_word();
+}
+#ifdef MG_DEBUG
+#define MG_CHECK_INDEX(var, ok, safe, err, bit) \
+  if (!(ok)) {                                  \
+    atomicOr((err), (bit));                     \
+    (var) = (safe);                             \
+  }
+#else
+#define MG_CHECK_INDEX(var, ok, safe, err, bit)
+#endif

@@ -19,9 +19,10 @@ size_t layernorm_bwd_workspace(int M, int D);
 
 // embedding.hip
 void embedding_fwd(const int64_t* idx, const bf16_t* wte, const bf16_t* wpe, bf16_t* out, int M,
-                   int T, int D, float p, uint64_t seed, hipStream_t stream);
+                   int T, int D, int V, float p, uint64_t seed, hipStream_t stream);
+unsigned int debug_error_bits();  // MG_DEBUG builds: device range-check bits, cleared on read
 void embedding_bwd(const int64_t* idx, const bf16_t* dout, float* dwte, float* dwpe, int M, int T,
-                   int D, float p, uint64_t seed, hipStream_t stream);
+                   int D, int V, float p, uint64_t seed, hipStream_t stream);
 
 // xent.hip
 void xent_fwd(const bf16_t* logits, const int64_t* targets, float* loss_row, float* lse, float* out,

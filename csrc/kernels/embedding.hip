@@ -18,14 +18,16 @@ namespace {
 __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict__ idx,
                                                       const bf16_t* __restrict__ wte,
                                                       const bf16_t* __restrict__ wpe,
-                                                      bf16_t* __restrict__ out, int M, int T, int D,
+                                                      bf16_t* __restrict__ out, int M, int T, int D, int V,
+                                                      unsigned int* __restrict__ err,
                                                       uint64_t seed, uint32_t thr, float scale,
                                                       int use_dropout, const uint64_t* sofs) {
   const int lane = threadIdx.x & 63;
   const long m = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= M) return;
   seed = eff_seed(seed, sofs);
-  const long tok = idx[m];
+  long tok = idx[m];
+  MG_CHECK_INDEX(tok, tok >= 0 && tok < V, 0, err, 1u)
   const int t = (int)(m % T);
   for (int c = lane * 8; c < D; c += 512) {
     float a[8], p[8];
@@ -40,14 +42,16 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict_
 
 __global__ __launch_bounds__(256) void emb_bwd_wte_kernel(const int64_t* __restrict__ idx,
                                                           const bf16_t* __restrict__ dout,
-                                                          float* __restrict__ dwte, int M, int D,
+                                                          float* __restrict__ dwte, int M, int D, int V,
+                                                          unsigned int* __restrict__ err,
                                                           uint64_t seed, uint32_t thr, float scale,
                                                           int use_dropout, const uint64_t* sofs) {
   const int lane = threadIdx.x & 63;
   const long m = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= M) return;
   seed = eff_seed(seed, sofs);
-  const long tok = idx[m];
+  long tok = idx[m];
+  MG_CHECK_INDEX(tok, tok >= 0 && tok < V, 0, err, 2u)
   // 8 columns per lane for the load, then 8 atomic instructions each covering 64 x 4 B contiguous.
   for (int c0 = 0; c0 < D; c0 += 512) {
     const int c = c0 + lane * 8;
@@ -102,25 +106,51 @@ __global__ __launch_bounds__(64) void emb_bwd_wpe_kernel(const bf16_t* __restric
 namespace mg {
 
 void embedding_fwd(const int64_t* idx, const bf16_t* wte, const bf16_t* wpe, bf16_t* out, int M,
-                   int T, int D, float p, uint64_t seed, hipStream_t stream) {
+                   int T, int D, int V, float p, uint64_t seed, hipStream_t stream) {
   const uint32_t thr = dropout_threshold8(p);  // the 8-bit residual-stream mask (common.h)
-  emb_fwd_kernel<<<cdiv(M, 4), 256, 0, stream>>>(idx, wte, wpe, out, M, T, D, seed, thr,
+  emb_fwd_kernel<<<cdiv(M, 4), 256, 0, stream>>>(idx, wte, wpe, out, M, T, D, V, debug_err_word(), seed, thr,
                                                  dropout_scale8(thr), p > 0.f,
                                                  graph_seed_ofs());
 }
 
 void embedding_bwd(const int64_t* idx, const bf16_t* dout, float* dwte, float* dwpe, int M, int T,
-                   int D, float p, uint64_t seed, hipStream_t stream) {
+                   int D, int V, float p, uint64_t seed, hipStream_t stream) {
   const uint32_t thr = dropout_threshold8(p);
   const float scale = dropout_scale8(thr);
   if (dwte)
-    emb_bwd_wte_kernel<<<cdiv(M, 4), 256, 0, stream>>>(idx, dout, dwte, M, D, seed, thr, scale,
+    emb_bwd_wte_kernel<<<cdiv(M, 4), 256, 0, stream>>>(idx, dout, dwte, M, D, V, debug_err_word(), seed, thr, scale,
                                                        p > 0.f, graph_seed_ofs());
   if (dwpe) {
     dim3 grid(T, cdiv(D, 512));
     emb_bwd_wpe_kernel<<<grid, 64, 0, stream>>>(dout, dwpe, M / T, T, D, seed, thr, scale, p > 0.f,
                                                 graph_seed_ofs());
   }
+}
+
+unsigned int* debug_err_word() {
+#ifdef MG_DEBUG
+  static unsigned int* w = nullptr;
+  if (!w) {
+    (void)hipMalloc(&w, sizeof(unsigned int));
+    (void)hipMemset(w, 0, sizeof(unsigned int));
+  }
+  return w;
+#else
+  return nullptr;
+#endif
+}
+
+unsigned int debug_error_bits() {
+#ifdef MG_DEBUG
+  unsigned int v = 0u;
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpy(&v, debug_err_word(), sizeof(v), hipMemcpyDeviceToHost);
+  (void)hipMemset(debug_err_word(), 0, sizeof(v));
+  (void)hipDeviceSynchronize();
+  return v;
+#else
+  return 0u;
+#endif
 }
 
 }  // namespace mg

@@ -20,7 +20,8 @@ namespace {
 __global__ __launch_bounds__(256) void xent_fwd_kernel(const bf16_t* __restrict__ logits,
                                                        const int64_t* __restrict__ targets,
                                                        float* __restrict__ loss_row,
-                                                       float* __restrict__ lse_out, int V, int ld) {
+                                                       float* __restrict__ lse_out, int V, int ld,
+                                                       unsigned int* __restrict__ err) {
   __shared__ float red[8];
   const long row = blockIdx.x;
   const bf16_t* lr = logits + row * ld;
@@ -53,7 +54,8 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(const bf16_t* __restrict_
   if (threadIdx.x == 0) {
     const float lse = gmx + __logf(gsm);
     lse_out[row] = lse;
-    const long t = targets[row];
+    long t = targets[row];
+  MG_CHECK_INDEX(t, t < V, -1, err, 4u)  // a target >= V would read past the row
     loss_row[row] = (t < 0) ? 0.f : lse - bf2f(lr[t]);
   }
 }
@@ -82,9 +84,11 @@ __global__ __launch_bounds__(256) void xent_bwd_kernel(const bf16_t* __restrict_
                                                        const float* __restrict__ lse,
                                                        const float* __restrict__ gscale,
                                                        const float* __restrict__ inv_n,
-                                                       bf16_t* __restrict__ dlogits, int V, int ld) {
+                                                       bf16_t* __restrict__ dlogits, int V, int ld,
+                                                       unsigned int* __restrict__ err) {
   const long row = blockIdx.x;
-  const long t = targets[row];
+  long t = targets[row];
+  MG_CHECK_INDEX(t, t < V, -1, err, 4u)  // a target >= V would read past the row
   const float g = (t < 0) ? 0.f : gscale[0] * inv_n[0];
   const float l = lse[row];
   const bf16_t* lr = logits + row * ld;
@@ -130,7 +134,7 @@ __global__ __launch_bounds__(1024) void xent_fused_kernel(const bf16_t* __restri
                                                           const float* __restrict__ inv_n,
                                                           float* __restrict__ loss_row,
                                                           bf16_t* __restrict__ dlogits, int V,
-                                                          int ld) {
+                                                          int ld, unsigned int* __restrict__ err) {
   __shared__ float red[32];
   const long row = blockIdx.x;
   const bf16_t* lr = logits + row * ld;
@@ -176,7 +180,8 @@ __global__ __launch_bounds__(1024) void xent_fused_kernel(const bf16_t* __restri
 #pragma unroll
   for (int k = 0; k < NV; ++k) reg_fence(u[k]);
   const float lse = gmx + __logf(gsm);
-  const long t = targets[row];
+  long t = targets[row];
+  MG_CHECK_INDEX(t, t < V, -1, err, 4u)  // a target >= V would read past the row
   const float g = (t < 0) ? 0.f : inv_n[0];
   const float lb = lse * L2E;
 #pragma unroll
@@ -213,13 +218,13 @@ namespace mg {
 
 void xent_fwd(const bf16_t* logits, const int64_t* targets, float* loss_row, float* lse, float* out,
               int M, int V, int ld, hipStream_t stream) {
-  xent_fwd_kernel<<<M, 256, 0, stream>>>(logits, targets, loss_row, lse, V, ld);
+  xent_fwd_kernel<<<M, 256, 0, stream>>>(logits, targets, loss_row, lse, V, ld, debug_err_word());
   xent_finalize_kernel<<<1, 1024, 0, stream>>>(loss_row, targets, out, M);
 }
 
 void xent_bwd(const bf16_t* logits, const int64_t* targets, const float* lse, const float* gscale,
               const float* inv_n, bf16_t* dlogits, int M, int V, int ld, hipStream_t stream) {
-  xent_bwd_kernel<<<M, 256, 0, stream>>>(logits, targets, lse, gscale, inv_n, dlogits, V, ld);
+  xent_bwd_kernel<<<M, 256, 0, stream>>>(logits, targets, lse, gscale, inv_n, dlogits, V, ld, debug_err_word());
 }
 
 }  // namespace mg
@@ -236,7 +241,7 @@ void xent_fused(const bf16_t* logits, const int64_t* targets, float* loss_row, f
   xent_count_kernel<<<1, 1024, 0, stream>>>(targets, out, M);
   switch (xent_fused_nv(ld)) {
 #define MG_XF(n) \
-  case n: xent_fused_kernel<n><<<M, 1024, 0, stream>>>(logits, targets, out + 1, loss_row, dlogits, V, ld); break;
+  case n: xent_fused_kernel<n><<<M, 1024, 0, stream>>>(logits, targets, out + 1, loss_row, dlogits, V, ld, debug_err_word()); break;
     MG_XF(4) MG_XF(5) MG_XF(6) MG_XF(7) MG_XF(8)
 #undef MG_XF
     default: break;

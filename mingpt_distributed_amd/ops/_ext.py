@@ -2,6 +2,12 @@
 
 GPU code paths call :func:`ext` which raises loudly if the extension is missing: there is no
 silent eager fallback for a GPU tensor.  CPU tensors never reach the extension.
+
+Debug mode: ``MINGPT_DEBUG_CHECKS=1`` wraps every extension entry point so the
+device is synchronised after it and a HIP error or a device range-check hit is raised *at that
+op*, named (the launch-blocking analogue).  With the ``-DMG_DEBUG`` build
+(``python build_ext.py --debug``, ``MINGPT_EXT_SO=build/debug/_C.so``) the kernels also
+range-check token ids and targets, clamp bad ones (no fault) and report them here.
 """
 from __future__ import annotations
 
@@ -31,6 +37,44 @@ def _load():
         _ERR = e
 
 
+_ERR_BITS = {1: "embedding_fwd: token id outside [0, vocab)",
+             2: "embedding_bwd: token id outside [0, vocab)",
+             4: "cross-entropy: target >= vocab"}
+
+
+class DeviceCheckError(RuntimeError):
+    """A device-side range check (MG_DEBUG build) or a HIP error, attributed to one op."""
+
+
+class _Checked:
+    """Extension proxy: synchronise after each call and raise on HIP errors / range-check bits."""
+
+    def __init__(self, mod):
+        self._mod = mod
+
+    def __getattr__(self, name):
+        fn = getattr(self._mod, name)
+        if not callable(fn) or name in ("debug_error_bits", "debug_build"):
+            return fn
+        mod = self._mod
+
+        def checked(*args, **kw):
+            import torch
+
+            out = fn(*args, **kw)
+            try:
+                torch.cuda.synchronize()
+            except RuntimeError as e:
+                raise DeviceCheckError(f"{name}: HIP error after the launch: {e}") from e
+            bits = int(mod.debug_error_bits())
+            if bits:
+                what = "; ".join(m for b, m in _ERR_BITS.items() if bits & b)
+                raise DeviceCheckError(f"{name}: device range check failed ({what})")
+            return out
+
+        return checked
+
+
 def available() -> bool:
     _load()
     return _EXT is not None
@@ -42,6 +86,8 @@ def ext():
         raise RuntimeError(
             "mingpt_distributed_amd._C (the gfx950 HIP extension) is not built or failed to load: "
             f"{_ERR!r}. Run `python build_ext.py` (hipcc --offload-arch=gfx950).")
+    if os.environ.get("MINGPT_DEBUG_CHECKS", "0") not in ("", "0"):
+        return _Checked(_EXT)
     return _EXT
 
 
