@@ -40,6 +40,9 @@ from .utils.config import CfgNode
 
 
 # ====================================================================================== engine
+_ROCTX = os.environ.get("MINGPT_ROCTX", "0") not in ("", "0")
+
+
 def _fold_grad(p):
     if p.grad is not None:
         p.main_grad.add_(p.grad.to(p.main_grad.dtype))
@@ -114,6 +117,10 @@ class StepEngine:
         return t.to(self.device, non_blocking=True)
 
     def _range(self, name: str):
+        if _ROCTX and self.device.type == "cuda":
+            # roctx ranges (torch.cuda.nvtx is roctx on ROCm): step phases show up as named
+            # ranges in `rocprofv3 --marker-trace` next to the kernel trace
+            return torch.cuda.nvtx.range(name)
         return torch.profiler.record_function(name) if self.annotate else contextlib.nullcontext()
 
     def forward_backward(self, x, y, scale: float = 1.0, sync: bool = True):
