@@ -69,3 +69,10 @@ hydra: {run: {dir: ./}}
     assert rc.data_config.train_split == 0.9  # D13: default when the YAML omits it
     with pytest.raises(KeyError):
         load_run_config(str(y), ["gpt_config.nonsense=1"])
+
+
+def test_zero1_override_reaches_trainer_config():
+    from mingpt_distributed_amd.utils.config import load_run_config
+
+    assert load_run_config(None, ["trainer_config.zero1=true"]).trainer_config.zero1 is True
+    assert load_run_config(None, []).trainer_config.zero1 is False
