@@ -10,6 +10,10 @@ reference's dropout (0.1) active.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--model gpt2]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
+``--gpus N > 1`` without a torchrun env starts the N ranks itself (a child
+``torch.distributed.run``); a rank whose process group is not N wide exits non-zero instead of
+reporting a smaller run under the requested GPU count.
+
 W untimed warmup steps, then K steps bracketed by barrier + device sync; the max over ranks is
 reported.  ``vs_baseline`` divides by N x the measured single-GPU torch-eager self-baseline of the
 same step at the same per-GPU batch, i.e. the per-GPU speedup over stock
@@ -18,6 +22,8 @@ PyTorch-ROCm (the reference publishes no numbers).
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,6 +35,27 @@ import torch
 # (bench/baseline_torch.py: torch.autocast bf16, SDPA attention, torch AdamW, MI355X):
 # BASELINE.md "Self-baseline" table.
 BASELINE_TOK_S_PER_GPU = {16: 367595.5, 32: 413092.9, 64: 461947.8}
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def _launch_ranks(n: int) -> int:
+    """``--gpus N`` without a torchrun env: start N rank processes (one per GPU) as a CHILD
+    ``torch.distributed.run`` and return its exit code.  Runs before anything touches the GPU
+    (``torch.cuda.device_count()`` does not initialise HIP on this image); never execs."""
+    have = torch.cuda.device_count()
+    if have < n:
+        print(f"bench.py: --gpus {n} requested but only {have} GPU(s) are visible", file=sys.stderr)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    print(f"bench.py: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
 
 
 def main():
@@ -43,30 +70,37 @@ def main():
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--vocab", type=int, default=50257, help="65 = chargpt's character vocabulary")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--reduce-dtype", default="bf16", choices=["fp32", "bf16"],
+                    help="gradient dtype on the wire for N > 1 (bf16: half the xGMI bytes)")
     ap.add_argument("--zero1", action="store_true",
                     help="shard the AdamW state over the ranks (reduce-scatter + all-gather)")
     ap.add_argument("--profile", default="", help="write a torch.profiler trace to this dir")
     ap.add_argument("--graph", action="store_true",
                     help="replay each step as one hipGraph (single GPU; StepEngine.graph_step)")
     a = ap.parse_args()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_launch_ranks(a.gpus))  # parent: no GPU call happens in this process
 
     from mingpt_distributed_amd.models import GPT, GPTConfig
     from mingpt_distributed_amd.parallel import dist as D
     from mingpt_distributed_amd.trainer import StepEngine
 
     info = D.init_distributed(device="cuda")
-    if info.world_size != a.gpus:
-        if info.rank == 0:
-            print(f"warning: --gpus {a.gpus} but WORLD_SIZE={info.world_size}; using WORLD_SIZE",
-                  file=sys.stderr)
-    N = info.world_size
+    N = D.world_size()  # from the process group itself, not the env
+    if N != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but the process group has {N} rank(s); refusing to "
+              f"report a {N}-GPU number as a {a.gpus}-GPU one", file=sys.stderr)
+        sys.exit(3)
+    print(f"[rank {info.rank}/{N}] local_rank {info.local_rank} on {torch.cuda.get_device_name(info.device)} "
+          f"({info.device}), backend {info.backend}", file=sys.stderr, flush=True)
     torch.manual_seed(1234 + info.rank)
     cfg = GPTConfig(model_type=a.model, vocab_size=a.vocab, block_size=a.seq, embed_drop=a.dropout,
                     resid_drop=a.dropout, attn_drop=a.dropout)
     torch.manual_seed(1234)  # identical init on every rank (the engine also broadcasts rank 0)
     model = GPT(cfg, verbose=info.rank == 0)
     eng = StepEngine(model, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, grad_clip=1.0,
-                     bucket_mb=a.bucket_mb, zero1=a.zero1)
+                     bucket_mb=a.bucket_mb, zero1=a.zero1,
+                     reduce_dtype=torch.bfloat16 if a.reduce_dtype == "bf16" else None)
     g = torch.Generator(device=eng.device).manual_seed(99 + info.rank)
     nb = 4
     xs = [torch.randint(0, a.vocab, (a.batch, a.seq), device=eng.device, generator=g) for _ in range(nb)]
@@ -117,7 +151,8 @@ def main():
             "data": "synthetic (random tokens, random-init weights)",
             "config": {"model": a.model, "global_batch": a.batch * N, "seq_len": a.seq,
                        "parallelism": f"dp{N}" + ("-zero1" if eng.zero1 else ""), "micro_batch_per_gpu": a.batch, "dropout": a.dropout,
-                       "bucket_mb": a.bucket_mb, "hip_graph": bool(a.graph and N == 1)},
+                       "bucket_mb": a.bucket_mb, "grad_reduce_dtype": a.reduce_dtype if N > 1 else None,
+                       "hip_graph": bool(a.graph and N == 1)},
             "loss": round(loss_v, 4),
             "max_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2),
         }

@@ -172,23 +172,53 @@ void grad_sumsq(const at::Tensor& grad, double grad_scale, const at::Tensor& out
   mg::grad_sumsq(fp(grad), grad.numel(), (float)grad_scale, fp(ws), fp(out), cur_stream());
 }
 
+// The chunk tables are built (and range-checked against these buffers) by optim.py at
+// construction; here: dtypes, sizes and the table lengths.
+void grad_sumsq_chunks(const at::Tensor& chunk_start, const at::Tensor& chunk_len,
+                       const at::Tensor& grad, double grad_scale, const at::Tensor& out) {
+  CHECK_I64(chunk_start); CHECK_DEV(chunk_len); CHECK_CONTIG(grad); CHECK_F32(out);
+  TORCH_CHECK(chunk_len.scalar_type() == at::kInt, "chunk_len must be int32");
+  TORCH_CHECK(grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16,
+              "grad must be fp32 or bf16");
+  TORCH_CHECK(chunk_start.numel() == chunk_len.numel() && out.numel() >= 2);
+  const int64_t nc = chunk_len.numel();
+  if (nc == 0) { out.zero_(); return; }
+  DevGuard g(grad.device());
+  auto ws = at::empty({nc}, out.options());
+  mg::grad_sumsq_chunks(chunk_start.data_ptr<int64_t>(), chunk_len.data_ptr<int>(), (int)nc,
+                        grad.data_ptr(), grad.scalar_type() == at::kBFloat16, (float)grad_scale,
+                        fp(ws), fp(out), cur_stream());
+}
+
 void adamw_step(const at::Tensor& chunk_start, const at::Tensor& chunk_len,
-                const at::Tensor& chunk_wd, const at::Tensor& master, const at::Tensor& param,
-                const at::Tensor& grad, const at::Tensor& m, const at::Tensor& v,
-                const at::Tensor& norm, double lr, double b1, double b2, double eps, int64_t step,
-                double grad_scale, double clip) {
+                const at::Tensor& chunk_wd, const c10::optional<at::Tensor>& moment_start,
+                const at::Tensor& master, const at::Tensor& param, const at::Tensor& grad,
+                const at::Tensor& m, const at::Tensor& v, const at::Tensor& norm, double lr,
+                double b1, double b2, double eps, int64_t step, double grad_scale, double clip) {
   CHECK_I64(chunk_start); CHECK_DEV(chunk_len); CHECK_F32(chunk_wd);
   TORCH_CHECK(chunk_len.scalar_type() == at::kInt, "chunk_len must be int32");
-  CHECK_F32(master); CHECK_BF16(param); CHECK_F32(grad); CHECK_F32(m); CHECK_F32(v); CHECK_F32(norm);
+  CHECK_F32(master); CHECK_BF16(param); CHECK_F32(m); CHECK_F32(v); CHECK_F32(norm);
+  CHECK_DEV(grad);
+  TORCH_CHECK(grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16,
+              "grad must be fp32 or bf16");
   const int64_t n = master.numel();
-  TORCH_CHECK(param.numel() == n && grad.numel() == n && m.numel() == n && v.numel() == n,
-              "adamw: flat buffer size mismatch");
+  TORCH_CHECK(param.numel() == n && grad.numel() == n, "adamw: flat buffer size mismatch");
+  const int64_t* ms = nullptr;
+  if (moment_start.has_value() && moment_start->defined()) {
+    CHECK_I64(*moment_start);
+    TORCH_CHECK(moment_start->numel() == chunk_start.numel(), "adamw: moment table length");
+    TORCH_CHECK(m.numel() == v.numel(), "adamw: moment buffer size mismatch");
+    ms = moment_start->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(m.numel() == n && v.numel() == n, "adamw: moment buffer size mismatch");
+  }
   TORCH_CHECK(chunk_start.numel() == chunk_len.numel() && chunk_wd.numel() == chunk_len.numel());
+  if (chunk_len.numel() == 0) return;
   DevGuard g(master.device());
-  mg::adamw_step(chunk_start.data_ptr<int64_t>(), chunk_len.data_ptr<int>(), fp(chunk_wd),
-                 (int)chunk_len.numel(), fp(master), bp(param), fp(grad), fp(m), fp(v), fp(norm),
-                 (float)lr, (float)b1, (float)b2, (float)eps, (int)step, (float)grad_scale,
-                 (float)clip, cur_stream());
+  mg::adamw_step(chunk_start.data_ptr<int64_t>(), chunk_len.data_ptr<int>(), fp(chunk_wd), ms,
+                 (int)chunk_len.numel(), fp(master), bp(param), grad.data_ptr(),
+                 grad.scalar_type() == at::kBFloat16, fp(m), fp(v), fp(norm), (float)lr, (float)b1,
+                 (float)b2, (float)eps, (int)step, (float)grad_scale, (float)clip, cur_stream());
 }
 
 void f32_to_bf16(const at::Tensor& src, const at::Tensor& dst) {
@@ -459,6 +489,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xent_scale_", &xent_scale_);
   m.def("set_graph_state", &set_graph_state, py::arg("seed_ofs") = py::none(), py::arg("opt_hp") = py::none());
   m.def("grad_sumsq", &grad_sumsq);
+  m.def("grad_sumsq_chunks", &grad_sumsq_chunks);
   m.def("adamw_step", &adamw_step);
   m.def("f32_to_bf16", &f32_to_bf16);
   m.def("bias_act", &bias_act);

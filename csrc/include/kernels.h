@@ -41,10 +41,14 @@ const float* graph_opt_hp();
 size_t grad_norm_workspace();
 void grad_sumsq(const float* grad, long n, float grad_scale, float* workspace, float* out,
                 hipStream_t stream);
-void adamw_step(const int64_t* chunk_start, const int* chunk_len, const float* chunk_wd, int n_chunks,
-                float* master, bf16_t* param, const float* grad, float* m, float* v,
-                const float* norm, float lr, float b1, float b2, float eps, int step,
-                float grad_scale, float clip, hipStream_t stream);
+void grad_sumsq_chunks(const int64_t* chunk_start, const int* chunk_len, int n_chunks,
+                       const void* grad, bool grad_bf16, float grad_scale, float* workspace,
+                       float* out, hipStream_t stream);
+void adamw_step(const int64_t* chunk_start, const int* chunk_len, const float* chunk_wd,
+                const int64_t* moment_start, int n_chunks, float* master, bf16_t* param,
+                const void* grad, bool grad_bf16, float* m, float* v, const float* norm, float lr,
+                float b1, float b2, float eps, int step, float grad_scale, float clip,
+                hipStream_t stream);
 void f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t stream);
 
 // gemv.hip (decode-time skinny GEMM, B <= 8 rows; epi 0 none, 1 bias, 2 bias+GELU, 3 bias+residual)

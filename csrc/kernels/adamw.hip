@@ -47,18 +47,64 @@ __global__ __launch_bounds__(256) void sumsq_final_kernel(const float* __restric
   }
 }
 
+// Gradient loads: fp32 main grads, or the bf16 buffer a bf16 all-reduce / reduce-scatter left.
+MG_DEVICE void load_grad4(const float* g, long e, float (&o)[4]) {
+  const float4 v = *reinterpret_cast<const float4*>(g + e);
+  o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+}
+MG_DEVICE void load_grad4(const bf16_t* g, long e, float (&o)[4]) {
+  const uint2 u = *reinterpret_cast<const uint2*>(g + e);
+  o[0] = bf2f(u.x & 0xffffu); o[1] = bf2f(u.x >> 16);
+  o[2] = bf2f(u.y & 0xffffu); o[3] = bf2f(u.y >> 16);
+}
+MG_DEVICE float load_grad1(const float* g, long e) { return g[e]; }
+MG_DEVICE float load_grad1(const bf16_t* g, long e) { return bf2f(g[e]); }
+
+// Sum of squares over the chunks of a chunk table (block b -> chunk b): the global grad norm of
+// exactly the elements the optimizer updates (a ZeRO shard is a set of pieces, not one range).
+template <typename G>
+__global__ __launch_bounds__(256) void sumsq_chunks_kernel(const int64_t* __restrict__ chunk_start,
+                                                           const int* __restrict__ chunk_len,
+                                                           const G* __restrict__ g,
+                                                           float* __restrict__ part) {
+  __shared__ float red[4];
+  const long s0 = chunk_start[blockIdx.x];
+  const int len = chunk_len[blockIdx.x];
+  float s = 0.f;
+  for (int i = threadIdx.x * 4; i < len; i += 256 * 4) {
+    if (i + 4 <= len) {
+      float v[4];
+      load_grad4(g, s0 + i, v);
+      s += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+    } else {
+      for (int j = i; j < len; ++j) {
+        const float v = load_grad1(g, s0 + j);
+        s += v * v;
+      }
+    }
+  }
+  s = block_sum<4>(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// chunk b updates master/param/grad[chunk_start[b] ...] and the moments at
+// m/v[moment_start[b] ...] (moment_start == nullptr: the same index).  Replicated DP keeps
+// moments for the whole flat buffer; ZeRO-1 keeps them only for the rank's pieces, packed.
+template <typename G>
 __global__ __launch_bounds__(256) void adamw_kernel(
     const int64_t* __restrict__ chunk_start, const int* __restrict__ chunk_len,
-    const float* __restrict__ chunk_wd, float* __restrict__ master, bf16_t* __restrict__ param,
-    const float* __restrict__ grad, float* __restrict__ m, float* __restrict__ v,
-    const float* __restrict__ norm, float lr, float b1, float b2, float eps, float bc1,
-    float bc2_sqrt, float grad_scale, float clip, const float* __restrict__ hp) {
+    const float* __restrict__ chunk_wd, const int64_t* __restrict__ moment_start,
+    float* __restrict__ master, bf16_t* __restrict__ param, const G* __restrict__ grad,
+    float* __restrict__ m, float* __restrict__ v, const float* __restrict__ norm, float lr, float b1,
+    float b2, float eps, float bc1, float bc2_sqrt, float grad_scale, float clip,
+    const float* __restrict__ hp) {
   if (hp) {  // graph mode: {lr, step} from device memory (the host values were captured once)
     lr = hp[0];
     bc1 = 1.f - powf(b1, hp[1]);
     bc2_sqrt = sqrtf(1.f - powf(b2, hp[1]));
   }
   const long s0 = chunk_start[blockIdx.x];
+  const long ms0 = moment_start ? moment_start[blockIdx.x] : s0;
   const int len = chunk_len[blockIdx.x];
   const float wd = chunk_wd[blockIdx.x];
   float gs = grad_scale;
@@ -70,13 +116,14 @@ __global__ __launch_bounds__(256) void adamw_kernel(
   const float decay = 1.f - lr * wd;
   const float step = lr / bc1;
   for (int i = threadIdx.x * 4; i < len; i += 256 * 4) {
-    const long e = s0 + i;
+    const long e = s0 + i, me = ms0 + i;
     if (i + 4 <= len) {
       float4 p = *reinterpret_cast<float4*>(master + e);
-      const float4 g = *reinterpret_cast<const float4*>(grad + e);
-      float4 mm = *reinterpret_cast<float4*>(m + e);
-      float4 vv = *reinterpret_cast<float4*>(v + e);
-      float pa[4] = {p.x, p.y, p.z, p.w}, ga[4] = {g.x, g.y, g.z, g.w};
+      float ga[4];
+      load_grad4(grad, e, ga);
+      float4 mm = *reinterpret_cast<float4*>(m + me);
+      float4 vv = *reinterpret_cast<float4*>(v + me);
+      float pa[4] = {p.x, p.y, p.z, p.w};
       float ma[4] = {mm.x, mm.y, mm.z, mm.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -86,18 +133,18 @@ __global__ __launch_bounds__(256) void adamw_kernel(
         pa[j] = pa[j] * decay - step * ma[j] / (sqrtf(va[j]) / bc2_sqrt + eps);
       }
       *reinterpret_cast<float4*>(master + e) = make_float4(pa[0], pa[1], pa[2], pa[3]);
-      *reinterpret_cast<float4*>(m + e) = make_float4(ma[0], ma[1], ma[2], ma[3]);
-      *reinterpret_cast<float4*>(v + e) = make_float4(va[0], va[1], va[2], va[3]);
+      *reinterpret_cast<float4*>(m + me) = make_float4(ma[0], ma[1], ma[2], ma[3]);
+      *reinterpret_cast<float4*>(v + me) = make_float4(va[0], va[1], va[2], va[3]);
       *reinterpret_cast<uint2*>(param + e) = make_uint2(pack2(pa[0], pa[1]), pack2(pa[2], pa[3]));
     } else {
       for (int j = 0; j < 4 && i + j < len; ++j) {
-        const long k = e + j;
-        const float gg = grad[k] * gs;
-        const float mj = b1 * m[k] + (1.f - b1) * gg;
-        const float vj = b2 * v[k] + (1.f - b2) * gg * gg;
+        const long k = e + j, mk = me + j;
+        const float gg = load_grad1(grad, k) * gs;
+        const float mj = b1 * m[mk] + (1.f - b1) * gg;
+        const float vj = b2 * v[mk] + (1.f - b2) * gg * gg;
         const float pj = master[k] * decay - step * mj / (sqrtf(vj) / bc2_sqrt + eps);
-        m[k] = mj;
-        v[k] = vj;
+        m[mk] = mj;
+        v[mk] = vj;
         master[k] = pj;
         param[k] = f2bf(pj);
       }
@@ -134,15 +181,35 @@ void grad_sumsq(const float* grad, long n, float grad_scale, float* workspace, f
   sumsq_final_kernel<<<1, 256, 0, stream>>>(workspace, kNormBlocks, grad_scale, out);
 }
 
-void adamw_step(const int64_t* chunk_start, const int* chunk_len, const float* chunk_wd, int n_chunks,
-                float* master, bf16_t* param, const float* grad, float* m, float* v,
-                const float* norm, float lr, float b1, float b2, float eps, int step,
-                float grad_scale, float clip, hipStream_t stream) {
+void grad_sumsq_chunks(const int64_t* chunk_start, const int* chunk_len, int n_chunks,
+                       const void* grad, bool grad_bf16, float grad_scale, float* workspace,
+                       float* out, hipStream_t stream) {
+  if (grad_bf16)
+    sumsq_chunks_kernel<bf16_t><<<n_chunks, 256, 0, stream>>>(
+        chunk_start, chunk_len, static_cast<const bf16_t*>(grad), workspace);
+  else
+    sumsq_chunks_kernel<float><<<n_chunks, 256, 0, stream>>>(
+        chunk_start, chunk_len, static_cast<const float*>(grad), workspace);
+  sumsq_final_kernel<<<1, 256, 0, stream>>>(workspace, n_chunks, grad_scale, out);
+}
+
+void adamw_step(const int64_t* chunk_start, const int* chunk_len, const float* chunk_wd,
+                const int64_t* moment_start, int n_chunks, float* master, bf16_t* param,
+                const void* grad, bool grad_bf16, float* m, float* v, const float* norm, float lr,
+                float b1, float b2, float eps, int step, float grad_scale, float clip,
+                hipStream_t stream) {
   const float bc1 = 1.f - powf(b1, (float)step);
   const float bc2_sqrt = sqrtf(1.f - powf(b2, (float)step));
-  adamw_kernel<<<n_chunks, 256, 0, stream>>>(chunk_start, chunk_len, chunk_wd, master, param, grad,
-                                             m, v, norm, lr, b1, b2, eps, bc1, bc2_sqrt, grad_scale,
-                                             clip, g_opt_hp);
+  if (grad_bf16)
+    adamw_kernel<bf16_t><<<n_chunks, 256, 0, stream>>>(
+        chunk_start, chunk_len, chunk_wd, moment_start, master, param,
+        static_cast<const bf16_t*>(grad), m, v, norm, lr, b1, b2, eps, bc1, bc2_sqrt, grad_scale,
+        clip, g_opt_hp);
+  else
+    adamw_kernel<float><<<n_chunks, 256, 0, stream>>>(
+        chunk_start, chunk_len, chunk_wd, moment_start, master, param,
+        static_cast<const float*>(grad), m, v, norm, lr, b1, b2, eps, bc1, bc2_sqrt, grad_scale,
+        clip, g_opt_hp);
 }
 
 void f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t stream) {

@@ -104,6 +104,27 @@ class GPTConfig:
     def head_dim(self) -> int:
         return self.n_embed // self.n_head
 
+    # shapes the gfx950 kernels take (checked on the host before the first GPU launch)
+    GPU_MAX_HEAD_DIM = 64
+
+    def gpu_unsupported(self) -> Optional[str]:
+        """Why the GPU kernels cannot run this config, or None.  Every kernel reads rows in
+        16-byte (8 x bf16) vectors and the attention kernels are instantiated per head dim."""
+        if self.n_embed is None or self.n_head is None:
+            return "config not resolved"
+        hd = self.n_embed // self.n_head
+        if self.n_embed % 8:
+            return f"n_embed={self.n_embed} must be a multiple of 8 on the GPU"
+        if hd % 8 or hd > self.GPU_MAX_HEAD_DIM or hd & (hd - 1):
+            return (f"head dim {hd} (n_embed/n_head) must be a power of two in [8, "
+                    f"{self.GPU_MAX_HEAD_DIM}] on the GPU")
+        return None
+
+    def check_gpu_support(self) -> None:
+        why = self.gpu_unsupported()
+        if why is not None:
+            raise ValueError(f"GPTConfig not supported by the GPU kernels: {why}")
+
     def __repr__(self):
         kv = ", ".join(f"{f.name}={getattr(self, f.name)!r}" for f in dataclasses.fields(self))
         return f"GPTConfig({kv})"

@@ -85,13 +85,36 @@ class _CpuCache:
 
 
 # ------------------------------------------------------------------------------------ GPU
+def bf16_weights(model):
+    """bf16 view of every weight the decode kernels read, converted ONCE and cached on the model.
+
+    A model trained through the engine already holds bf16 compute weights (returned as is); an
+    fp32 model (e.g. ``from_pretrained`` without ``.to(bfloat16)``) gets one bf16 copy per
+    weight, reused across decode steps and ``generate`` calls, and refreshed only when the weight
+    changes (storage pointer or in-place version).  The captured decode hipGraph therefore holds
+    no conversion kernels: per-token traffic is the bf16 weights once."""
+    cache = model.__dict__.setdefault("_mg_bf16_weights", {})
+
+    def get(w: torch.Tensor) -> torch.Tensor:
+        if w.dtype == torch.bfloat16:
+            return w
+        stamp = (w.data_ptr(), w._version)
+        ent = cache.get(id(w))
+        if ent is None or ent[0] != stamp:
+            ent = (stamp, w.detach().to(torch.bfloat16).contiguous())
+            cache[id(w)] = ent
+        return ent[1]
+
+    return get
+
+
 class _GpuCache:
     def __init__(self, model, idx, tmax):
         from ..ops._ext import ext
         from ..ops import gemm as G
-        from ..ops.fused import _bf16
 
-        self.C, self.G, self.bf = ext(), G, _bf16
+        model.config.check_gpu_support()
+        self.C, self.G, self.bf = ext(), G, bf16_weights(model)
         self.model = model
         self.tmax = tmax
         B, T = idx.shape

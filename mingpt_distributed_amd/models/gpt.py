@@ -88,7 +88,7 @@ class Block(nn.Module):
         ps = [self.ln_1.weight, self.ln_1.bias, a.c_attn.weight, a.c_attn.bias, a.c_proj.weight,
               a.c_proj.bias, self.ln_2.weight, self.ln_2.bias, m.c_fc.weight, m.c_fc.bias,
               m.c_proj.weight, m.c_proj.bias]
-        y = TransformerBlockFn.apply(x.reshape(B * T, D), *[_bf16(p) for p in ps],
+        y = TransformerBlockFn.run(x.reshape(B * T, D), *[_bf16(p) for p in ps],
                                      (B, T, c.n_head, p_attn, p_resid, c.layer_norm_eps))
         return y.view(B, T, D)
 
@@ -184,19 +184,22 @@ class GPT(nn.Module):
         from ..ops.fused import EmbeddingFn, HeadFn, HeadLossFn, _bf16
 
         tr, c = self.transformer, self.config
+        if not getattr(self, "_gpu_checked", False):
+            c.check_gpu_support()  # before any launch, not mid-step
+            self._gpu_checked = True
         p = c.embed_drop if self.training else 0.0
-        x = EmbeddingFn.apply(idx, _bf16(tr.wte.weight), _bf16(tr.wpe.weight), p)
+        x = EmbeddingFn.run(idx, _bf16(tr.wte.weight), _bf16(tr.wpe.weight), p)
         for block in tr.h:
             x = block(x)
         B, T, D = x.shape
         x2 = x.reshape(B * T, D)
         V = self.config.vocab_size
         if targets is not None:
-            logits, loss = HeadLossFn.apply(x2, _bf16(tr.ln_f.weight), _bf16(tr.ln_f.bias),
+            logits, loss = HeadLossFn.run(x2, _bf16(tr.ln_f.weight), _bf16(tr.ln_f.bias),
                                             _bf16(self.lm_head.weight), targets.reshape(-1).contiguous(),
                                             c.layer_norm_eps)
             return logits.view(B, T, -1)[..., :V], loss
-        logits = HeadFn.apply(x2, _bf16(tr.ln_f.weight), _bf16(tr.ln_f.bias), _bf16(self.lm_head.weight),
+        logits = HeadFn.run(x2, _bf16(tr.ln_f.weight), _bf16(tr.ln_f.bias), _bf16(self.lm_head.weight),
                               c.layer_norm_eps)
         return logits.view(B, T, -1)[..., :V], None
 

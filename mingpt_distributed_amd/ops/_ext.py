@@ -62,6 +62,10 @@ class _Checked:
             import torch
 
             out = fn(*args, **kw)
+            if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                # inside a hipGraph capture (StepEngine.graph_step) a sync or a blocking read
+                # would invalidate the capture: the launch is checked when the graph replays
+                return out
             try:
                 torch.cuda.synchronize()
             except RuntimeError as e:

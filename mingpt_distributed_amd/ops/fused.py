@@ -19,7 +19,7 @@ import torch
 
 from . import gemm as G
 from ._ext import ext
-from .grads import finish, grad_target, note_use
+from .grads import before_use, finish, grad_target, note_use
 
 
 def new_seed() -> int:
@@ -70,16 +70,31 @@ def _wgrad(dy, x, main_grad):
         G.gemm_tn_acc(dy, x, main_grad)
 
 
-class EmbeddingFn(torch.autograd.Function):
+class _EngineFn(torch.autograd.Function):
+    """Autograd Function over engine-managed parameters.  Call :meth:`run`, not ``apply``: the
+    gradient-readiness protocol counts a parameter use only when the CALLER runs with grad
+    enabled, and inside ``forward`` autograd has always switched grad mode off (a use counted
+    there under ``no_grad`` would never be matched by a backward; one skipped there would let a
+    bucket holding a tied weight launch before its second gradient lands)."""
+
+    @classmethod
+    def run(cls, *args):
+        if torch.is_grad_enabled():
+            for a in args:
+                if isinstance(a, torch.Tensor) and a.requires_grad:
+                    note_use(a)
+        return cls.apply(*args)
+
+
+class EmbeddingFn(_EngineFn):
     @staticmethod
     def forward(ctx, idx, wte, wpe, p):
+        before_use(wte, wpe)
         seed = new_seed() if p > 0 else 0
         out = ext().embedding_fwd(idx.contiguous(), wte, wpe, float(p), seed)
         ctx.save_for_backward(idx)
         ctx.params = (wte, wpe)
         ctx.p, ctx.seed = p, seed
-        note_use(wte)
-        note_use(wpe)
         return out
 
     @staticmethod
@@ -93,13 +108,14 @@ class EmbeddingFn(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------------------------ block
-class TransformerBlockFn(torch.autograd.Function):
+class TransformerBlockFn(_EngineFn):
     """x [M, D] -> x + attn(ln1(x)) -> (+ mlp(ln2(.)))  with every op on a HIP kernel."""
 
     @staticmethod
     def forward(ctx, x, ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, wfc, bfc, wp, bp, cfg):
         B, T, H, p_attn, p_resid, eps = cfg
         C = ext()
+        before_use(ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, wfc, bfc, wp, bp)
         seeds = (new_seed() if p_attn > 0 else 0, new_seed() if p_resid > 0 else 0,
                  new_seed() if p_resid > 0 else 0)
         h, mean1, rstd1 = C.layernorm_fwd(x, ln1w, ln1b, eps)
@@ -116,8 +132,6 @@ class TransformerBlockFn(torch.autograd.Function):
         ctx.save_for_backward(x, h, mean1, rstd1, qkv, y, lse, amask, x1, h2, mean2, rstd2, gd, u)
         ctx.params = (ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, wfc, bfc, wp, bp)
         ctx.cfg, ctx.seeds = cfg, seeds
-        for prm in ctx.params:
-            note_use(prm)
         return x2
 
     @staticmethod
@@ -182,12 +196,13 @@ def _padded_weight(w, ld):
     return wp
 
 
-class HeadLossFn(torch.autograd.Function):
+class HeadLossFn(_EngineFn):
     """loss = CE(LN_f(x) @ W^T, targets) with padded-vocab logits; returns (logits[M, Vpad], loss)."""
 
     @staticmethod
     def forward(ctx, x, lnw, lnb, w, targets, eps):
         C = ext()
+        before_use(lnw, lnb, w)
         V = w.shape[0]
         ld = (V + 127) // 128 * 128
         h, mean, rstd = C.layernorm_fwd(x, lnw, lnb, eps)
@@ -207,8 +222,6 @@ class HeadLossFn(torch.autograd.Function):
         ctx.fused = bool(fused)
         ctx.params = (lnw, lnb, w)
         ctx.eps = eps
-        for prm in ctx.params:
-            note_use(prm)
         ctx.mark_non_differentiable(logits)
         ctx.set_materialize_grads(False)  # never build a [M, Vpad] zero grad for the logits
         return logits, out[0]
@@ -238,12 +251,13 @@ class HeadLossFn(torch.autograd.Function):
         return dx, finish(lnw, blw, mlw), finish(lnb, blb, mlb), finish(w, bw, mw), None, None
 
 
-class HeadFn(torch.autograd.Function):
+class HeadFn(_EngineFn):
     """logits = LN_f(x) @ W^T (inference / custom-loss path). Gradient flows to x and weights."""
 
     @staticmethod
     def forward(ctx, x, lnw, lnb, w, eps):
         C = ext()
+        before_use(lnw, lnb, w)
         V = w.shape[0]
         ld = (V + 7) // 8 * 8
         h, mean, rstd = C.layernorm_fwd(x, lnw, lnb, eps)
@@ -251,8 +265,6 @@ class HeadFn(torch.autograd.Function):
         ctx.save_for_backward(x, h, mean, rstd)
         ctx.params = (lnw, lnb, w)
         ctx.eps, ctx.ld = eps, ld
-        for prm in ctx.params:
-            note_use(prm)
         return logits
 
     @staticmethod

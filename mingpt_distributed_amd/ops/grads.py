@@ -20,9 +20,22 @@ def main_grad(p: torch.Tensor):
     return getattr(p, "main_grad", None)
 
 
+def before_use(*params: torch.Tensor) -> None:
+    """Call before launching kernels that read ``params``: under ZeRO-1 the compute stream waits
+    (stream-ordered, no host block) for the all-gather that brings those weights up to date, so
+    the gather of later layers overlaps the forward of earlier ones."""
+    for p in params:
+        eng = getattr(p, "_mg_engine", None)
+        if eng is not None:
+            eng.before_use(p)
+
+
 def note_use(p: torch.Tensor) -> None:
+    """Count one use of ``p`` whose gradient the coming backward will produce.  Call it where
+    the caller's grad mode is in force (``fused._EngineFn.run``), never inside
+    ``autograd.Function.forward`` (grad mode is always off there)."""
     eng = getattr(p, "_mg_engine", None)
-    if eng is not None and torch.is_grad_enabled() and p.requires_grad:
+    if eng is not None and p.requires_grad:
         eng.note_use(p)
 
 

@@ -67,36 +67,94 @@ def create_optimizer(model: nn.Module, optimizer_config) -> torch.optim.AdamW:
                              eps=getattr(optimizer_config, "eps", 1e-8))
 
 
+def _round_up(n: int, m: int) -> int:
+    return (n + m - 1) // m * m
+
+
+def make_chunk_table(pieces, device, bound: int, moment_bound: Optional[int] = None):
+    """Kernel chunk table from ``pieces`` = [(start, end, wd, moment_start)] of flat-buffer ranges:
+    CHUNK-sized chunks (one workgroup each) that never straddle a piece, so weight decay is a
+    per-chunk constant.  Every range is checked against the buffers here, on the host, because
+    the kernels index the flat buffers through these tables unchecked."""
+    starts, lens, wds, mstarts = [], [], [], []
+    for a, b, wd, ma in pieces:
+        if not (0 <= a <= b <= bound) or a % 4 or (ma is not None and (ma % 4 or ma + (b - a) > moment_bound)):
+            raise ValueError(f"chunk piece [{a}, {b}) (moments at {ma}) outside the flat buffers")
+        for c in range(a, b, CHUNK):
+            starts.append(c)
+            lens.append(min(CHUNK, b - c))
+            wds.append(wd)
+            mstarts.append(c - a + (a if ma is None else ma))
+    t = dict(device=device)
+    return (torch.tensor(starts, dtype=torch.int64, **t), torch.tensor(lens, dtype=torch.int32, **t),
+            torch.tensor(wds, dtype=torch.float32, **t), torch.tensor(mstarts, dtype=torch.int64, **t))
+
+
 class FlatParamStore:
-    """All parameters of ``model`` as views into flat buffers (see module docstring)."""
+    """All parameters of ``model`` as views into flat buffers (see module docstring).
+
+    ``bucket_numel`` cuts the layout into communication buckets: runs of whole parameters of at
+    least that many elements, each padded to a multiple of ``bucket_align`` (the DP engine
+    all-reduces a bucket as one contiguous slice; ZeRO-1 pads every bucket to ``world * 64`` so
+    it splits into equal, aligned rank shards).  ``order`` (parameter names) fixes the layout
+    order -- the data-parallel engine rebuilds the store in the order gradients were observed to
+    complete -- and ``master_from`` initialises fp32 masters from another store by name."""
 
     def __init__(self, model: nn.Module, compute_dtype: Optional[torch.dtype] = None,
-                 device: Optional[torch.device] = None, pad_multiple: int = ALIGN):
+                 device: Optional[torch.device] = None, bucket_numel: Optional[int] = None,
+                 bucket_align: int = ALIGN, order: Optional[List[str]] = None,
+                 master_from: Optional["FlatParamStore"] = None):
         named = list(model.named_parameters())  # dedups tied weights
         if device is None:
             device = named[0][1].device
         device = torch.device(device)
         if compute_dtype is None:
             compute_dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
+        if bucket_align % ALIGN:
+            raise ValueError("bucket_align must be a multiple of 64 elements")
         self.device, self.compute_dtype = device, compute_dtype
+        seq = list(reversed(named))  # reverse registration order ~ backward completion order
+        if order is not None:
+            rank = {n: k for k, n in enumerate(order)}
+            seq.sort(key=lambda np_: rank.get(np_[0], len(rank)))  # stable: unknown names last
         self.names: List[str] = []
         self.params: List[nn.Parameter] = []
         self.offsets: List[int] = []
         self.numels: List[int] = []
-        off = 0
-        for name, p in reversed(named):
+        self.buckets: List[Tuple[int, int, List[int]]] = []
+        off, bstart, cur = 0, 0, []
+        for name, p in seq:
+            if bucket_numel is not None and cur and p.numel() >= bucket_numel:
+                # a parameter as large as a bucket gets a bucket of its own: the smaller
+                # gradients before it launch without waiting for it (e.g. GPT-2's tied wte)
+                off = _round_up(off, bucket_align)
+                self.buckets.append((bstart, off, cur))
+                bstart, cur = off, []
             self.names.append(name)
             self.params.append(p)
             self.offsets.append(off)
             self.numels.append(p.numel())
-            off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
-        # ZeRO-1 pads the tail so the buffer splits into equal, 64-element aligned rank shards
-        self.total = (off + pad_multiple - 1) // pad_multiple * pad_multiple
+            off += _round_up(p.numel(), ALIGN)
+            cur.append(len(self.params) - 1)
+            if bucket_numel is not None and off - bstart >= bucket_numel:
+                off = _round_up(off, bucket_align)
+                self.buckets.append((bstart, off, cur))
+                bstart, cur = off, []
+        if cur or not self.buckets:
+            off = _round_up(max(off, 1), bucket_align)
+            self.buckets.append((bstart, off, cur))
+        self.total = off
         f32 = dict(dtype=torch.float32, device=device)
         self.master = torch.zeros(self.total, **f32)
         self.grad = torch.zeros(self.total, **f32)
-        for p, o, n in zip(self.params, self.offsets, self.numels):
-            self.master[o:o + n].copy_(p.detach().reshape(-1).to(device=device, dtype=torch.float32))
+        src = {}
+        if master_from is not None:
+            src = {n: master_from.master[o:o + k] for n, o, k in
+                   zip(master_from.names, master_from.offsets, master_from.numels)}
+        for name, p, o, n in zip(self.names, self.params, self.offsets, self.numels):
+            v = src.get(name)
+            self.master[o:o + n].copy_(v if v is not None else
+                                       p.detach().reshape(-1).to(device=device, dtype=torch.float32))
         if compute_dtype == torch.float32:
             self.flat = self.master  # CPU / fp32 path: params ARE the master weights
         else:
@@ -106,6 +164,7 @@ class FlatParamStore:
             p.main_grad = self.grad[o:o + n].view(p.shape)
             p.grad = None
         self.index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
+        self.by_name: Dict[str, int] = {n: i for i, n in enumerate(self.names)}
 
     def views(self, buf: torch.Tensor) -> List[torch.Tensor]:
         return [buf[o:o + n].view(p.shape) for p, o, n in zip(self.params, self.offsets, self.numels)]
@@ -117,14 +176,15 @@ class FlatParamStore:
         if self.flat is not self.master:
             self.flat.copy_(self.master)
 
-    def chunk_table(self, wd_of: Dict[str, float]):
-        starts, lens, wds = [], [], []
+    def pieces(self, wd_of: Dict[str, float], lo: int = 0, hi: Optional[int] = None):
+        """(start, end, wd) of every parameter's elements inside the flat range [lo, hi)."""
+        hi = self.total if hi is None else hi
+        out = []
         for name, o, n in zip(self.names, self.offsets, self.numels):
-            for c in range(0, n, CHUNK):
-                starts.append(o + c)
-                lens.append(min(CHUNK, n - c))
-                wds.append(wd_of[name])
-        return starts, lens, wds
+            a, b = max(o, lo), min(o + n, hi)
+            if a < b:
+                out.append((a, b, wd_of[name]))
+        return out
 
 
 class FusedAdamW:
@@ -145,11 +205,12 @@ class FusedAdamW:
         self.exp_avg = torch.zeros(store.total, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(store.total, dtype=torch.float32, device=dev)
         self.norm_buf = torch.zeros(2, dtype=torch.float32, device=dev)
-        starts, lens, wds = store.chunk_table(self.wd_of)
-        self.n_chunks = len(starts)
-        self.c_start = torch.tensor(starts, dtype=torch.int64, device=dev)
-        self.c_len = torch.tensor(lens, dtype=torch.int32, device=dev)
-        self.c_wd = torch.tensor(wds, dtype=torch.float32, device=dev)
+        pieces = [(a, b, wd, None) for a, b, wd in store.pieces(self.wd_of)]
+        self.c_start, self.c_len, self.c_wd, _ = make_chunk_table(pieces, dev, store.total)
+        self.n_chunks = int(self.c_len.numel())
+        # where step() reads the (all-reduced) gradients: the fp32 main grads, or the bf16 buffer
+        # the data-parallel engine reduced them in (DataParallelEngine(reduce_dtype=bf16))
+        self.grad_buffer: torch.Tensor = store.grad
         # torch-optimizer look-alike for LR schedulers / logging
         self.param_groups = [{"lr": lr, "betas": self.betas, "weight_decay": weight_decay, "eps": eps}]
 
@@ -167,13 +228,13 @@ class FusedAdamW:
             from .ops._ext import ext
 
             C = ext()
-            C.grad_sumsq(s.grad, grad_scale, self.norm_buf)
-            C.adamw_step(self.c_start, self.c_len, self.c_wd, s.master, s.flat, s.grad, self.exp_avg,
-                         self.exp_avg_sq, self.norm_buf, lr, b1, b2, self.eps, self.step_count,
-                         grad_scale, float(self.grad_clip))
+            C.grad_sumsq_chunks(self.c_start, self.c_len, self.grad_buffer, grad_scale, self.norm_buf)
+            C.adamw_step(self.c_start, self.c_len, self.c_wd, None, s.master, s.flat, self.grad_buffer,
+                         self.exp_avg, self.exp_avg_sq, self.norm_buf, lr, b1, b2, self.eps,
+                         self.step_count, grad_scale, float(self.grad_clip))
             return
         # CPU path (plain PyTorch, same math)
-        g = s.grad * grad_scale
+        g = self.grad_buffer.float() * grad_scale
         sumsq = (g * g).sum()
         self.norm_buf[0] = sumsq
         self.norm_buf[1] = sumsq.sqrt()
@@ -221,3 +282,19 @@ class FusedAdamW:
 
     def zero_grad(self, set_to_none: bool = True):
         self.store.zero_grad()
+
+    def rehome(self, new_store: FlatParamStore):
+        """Move the moments to ``new_store``'s layout (same parameters, other order/padding)."""
+        old = self.store
+        m = torch.zeros(new_store.total, dtype=torch.float32, device=new_store.device)
+        v = torch.zeros_like(m)
+        for name, o, n in zip(old.names, old.offsets, old.numels):
+            k = new_store.by_name[name]
+            no = new_store.offsets[k]
+            m[no:no + n].copy_(self.exp_avg[o:o + n])
+            v[no:no + n].copy_(self.exp_avg_sq[o:o + n])
+        sd_step = self.step_count
+        self.__init__(new_store, lr=self.param_groups[0]["lr"], betas=self.betas, eps=self.eps,
+                      weight_decay=self.weight_decay, decay_names=self.decay_names,
+                      grad_clip=self.grad_clip)
+        self.exp_avg, self.exp_avg_sq, self.step_count = m, v, sd_step

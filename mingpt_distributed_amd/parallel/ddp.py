@@ -5,8 +5,9 @@ Replaces ``torch.nn.parallel.DistributedDataParallel`` as used by the reference
 for one node of 8 MI355X on a point-to-point xGMI mesh:
 
 * **Zero-copy buckets.**  Gradients live in the flat fp32 buffer of :class:`FlatParamStore`
-  (``p.main_grad`` views) in backward-completion order, so a bucket is a contiguous slice of that
-  buffer: no gradient->bucket copy and no copy back (DDP's K19 reducer copies).
+  (``p.main_grad`` views) in backward-completion order, and the store cuts that buffer into
+  buckets (``store.buckets``), so a bucket is a contiguous slice: no gradient->bucket copy and
+  no copy back (DDP's K19 reducer copies).
 * **Readiness by use counts.**  The fused GPU ops report each parameter use in forward and each
   gradient accumulation in backward (``ops/grads.py``); on the CPU path a
   ``post_accumulate_grad`` hook folds ``p.grad`` into ``main_grad``.  A bucket launches the
@@ -16,9 +17,20 @@ for one node of 8 MI355X on a point-to-point xGMI mesh:
   process group's own HIP stream, ordered after the compute-stream kernels that produced the
   bucket, while backward keeps issuing kernels on the compute stream.  ``finish()`` makes the
   compute stream wait on the outstanding collectives (no host block) before the optimizer.
+* **bf16 on the wire** (``reduce_dtype=torch.bfloat16``): a bucket is converted into a
+  persistent bf16 comm buffer by one kernel the moment it is ready, reduced there in place, and
+  the optimizer reads the reduced bf16 gradients directly (``FusedAdamW.grad_buffer``): half the
+  link bytes, no per-step allocation and no copy back to fp32.
+* **Bucket order from the observed backward.**  The first synchronised backward records the
+  order in which parameters became ready; if it differs from the layout (a model whose
+  registration order is not its reverse use order), :meth:`relayout_order` returns it and the
+  step engine rebuilds the store in that order after the first optimizer step, as DDP rebuilds
+  its buckets after iteration 1.
 * **Sizing.**  Default 32 MiB fp32 buckets: big enough that each ring all-reduce is bandwidth-
   rather than latency-bound on xGMI (7 links x ~153 GB/s per GPU), small enough that the first
-  bucket launches early in backward.  ``reduce_dtype=torch.bfloat16`` halves link bytes.
+  bucket launches early in backward.  The tied ``wte`` (its last use is the embedding backward,
+  the final kernel of backward) sits alone in the last bucket, so what is exposed after
+  backward is exactly that one reduction.
 * The average over ranks (1/world) is folded into the optimizer's grad scale; the constant
   causal mask is never broadcast (there is no mask buffer; fixes D30).
 """
@@ -34,38 +46,39 @@ from ..optim import FlatParamStore
 
 
 class _Bucket:
-    __slots__ = ("start", "end", "params", "ready", "launched", "work", "staging")
+    __slots__ = ("start", "end", "params", "ready", "work")
 
     def __init__(self, start, end, params):
         self.start, self.end, self.params = start, end, params
         self.ready = 0
-        self.launched = False
         self.work = None
-        self.staging = None
+
+
+def _to_bf16(src: torch.Tensor, dst: torch.Tensor):
+    if src.is_cuda:
+        from ..ops._ext import ext
+
+        ext().f32_to_bf16(src, dst)
+    else:
+        dst.copy_(src)
 
 
 class DataParallelEngine:
     def __init__(self, store: FlatParamStore, process_group=None, bucket_mb: float = 32.0,
-                 reduce_dtype: Optional[torch.dtype] = None, broadcast: bool = True):
+                 reduce_dtype: Optional[torch.dtype] = None, broadcast: bool = True,
+                 comm_at_world1: bool = False):
+        """``comm_at_world1`` runs the collective path even in a one-rank process group (tests
+        of the RCCL calls on a one-GPU box); otherwise one rank means no communication."""
         self.store = store
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
-        self.reduce_dtype = reduce_dtype
+        self.active = self.world > 1 or (comm_at_world1 and dist.is_initialized())
+        if reduce_dtype not in (None, torch.float32, torch.bfloat16):
+            raise ValueError("reduce_dtype must be None/float32 or bfloat16")
+        self.reduce_dtype = None if reduce_dtype == torch.float32 else reduce_dtype
+        self.bucket_mb = bucket_mb
         self.sync_enabled = True
-        self.buckets: List[_Bucket] = []
-        cap = int(bucket_mb * 1024 * 1024 / 4)
-        cur: List[int] = []
-        start = 0
-        for i, (o, n) in enumerate(zip(store.offsets, store.numels)):
-            if not cur:
-                start = o
-            cur.append(i)
-            end = o + n
-            if end - start >= cap:
-                self.buckets.append(_Bucket(start, self._aligned_end(i), cur))
-                cur = []
-        if cur:
-            self.buckets.append(_Bucket(start, self._aligned_end(len(store.params) - 1), cur))
+        self.buckets: List[_Bucket] = [_Bucket(s, e, ps) for s, e, ps in store.buckets]
         self.bucket_of = {}
         for bi, b in enumerate(self.buckets):
             for i in b.params:
@@ -74,16 +87,26 @@ class DataParallelEngine:
         self.done = [False] * len(store.params)
         self.next_launch = 0
         self._hooks = []
-        if self.world > 1:
+        self.comm = None  # bf16 reduce buffer (same layout as store.grad)
+        self.observed: Optional[List[int]] = None  # ready order of the first synchronised backward
+        self._recording: Optional[List[int]] = []
+        if self.active:
+            if self.reduce_dtype is not None:
+                self.comm = torch.empty(store.total, dtype=self.reduce_dtype, device=store.device)
             for p in store.params:
                 p._mg_engine = self
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._cpu_grad_hook))
             if broadcast:
                 self.broadcast_params()
 
-    def _aligned_end(self, i):
-        s = self.store
-        return s.offsets[i + 1] if i + 1 < len(s.offsets) else s.total
+    @staticmethod
+    def bucket_numel(bucket_mb: float) -> int:
+        return max(1, int(bucket_mb * 1024 * 1024 / 4))
+
+    @property
+    def grad_buffer(self) -> torch.Tensor:
+        """The buffer holding the reduced gradients after :meth:`finish`."""
+        return self.comm if self.comm is not None else self.store.grad
 
     # ------------------------------------------------------------------ setup
     def broadcast_params(self, src: int = 0):
@@ -96,6 +119,9 @@ class DataParallelEngine:
         return 1.0 / self.world
 
     # ------------------------------------------------------------------ readiness protocol
+    def before_use(self, p):
+        """Called before a forward reads ``p`` (ZeRO-1 waits for its parameter gather here)."""
+
     def note_use(self, p):
         self.uses[self.store.index[id(p)]] += 1
 
@@ -115,6 +141,8 @@ class DataParallelEngine:
         if self.done[i]:
             return
         self.done[i] = True
+        if self.sync_enabled and self._recording is not None:
+            self._recording.append(i)
         b = self.buckets[self.bucket_of[i]]
         b.ready += 1
         if self.sync_enabled:
@@ -128,19 +156,29 @@ class DataParallelEngine:
             self._launch(b)
             self.next_launch += 1
 
-    def _launch(self, b: _Bucket):
+    def _wire(self, b: _Bucket) -> torch.Tensor:
+        """The bucket's slice in the dtype it travels in (converted now if bf16)."""
         view = self.store.grad[b.start:b.end]
-        if self.reduce_dtype is not None and self.reduce_dtype != view.dtype:
-            b.staging = view.to(self.reduce_dtype)
-            b.work = dist.all_reduce(b.staging, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
-        else:
-            b.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
-        b.launched = True
+        if self.comm is None:
+            return view
+        out = self.comm[b.start:b.end]
+        _to_bf16(view, out)
+        return out
+
+    def _launch(self, b: _Bucket):
+        b.work = dist.all_reduce(self._wire(b), op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     # ------------------------------------------------------------------ step boundary
+    def _wait_all(self):
+        for b in self.buckets:
+            if b.work is not None:
+                b.work.wait()  # stream-ordered: the compute stream waits, the host does not
+            b.work = None
+            b.ready = 0
+
     def finish(self):
         """Launch what is left (parameters unused this step), wait, and reset for the next step."""
-        if self.world == 1:
+        if not self.active:
             return
         if self.sync_enabled:
             for i in range(len(self.done)):
@@ -148,23 +186,29 @@ class DataParallelEngine:
                     self.done[i] = True
                     self.buckets[self.bucket_of[i]].ready += 1
             self._launch_ready()
-            for b in self.buckets:
-                if b.work is not None:
-                    b.work.wait()  # stream-ordered: the compute stream waits, the host does not
-                    if b.staging is not None:
-                        self.store.grad[b.start:b.end].copy_(b.staging)
-                        b.staging = None
-                b.work = None
-                b.launched = False
-                b.ready = 0
+            self._wait_all()
             self.next_launch = 0
-            self.done = [False] * len(self.done)
+            if self._recording is not None:
+                seen = set(self._recording)
+                self.observed = self._recording + [i for i in range(len(self.done)) if i not in seen]
+                self._recording = None
         else:
             # no_sync micro-step: keep counts clear for the next micro-step
             for b in self.buckets:
                 b.ready = 0
-            self.done = [False] * len(self.done)
+        self.done = [False] * len(self.done)
         self.uses = [0] * len(self.uses)
+
+    def relayout_order(self) -> Optional[List[str]]:
+        """Parameter names in observed gradient-ready order if that differs from the layout
+        (buckets would wait on late gradients), else None.  Consumed once."""
+        obs, self.observed = self.observed, None
+        if obs is None:
+            return None
+        seq = [self.bucket_of[i] for i in obs]
+        if all(a <= b for a, b in zip(seq, seq[1:])):
+            return None  # buckets complete in launch order; order inside a bucket is irrelevant
+        return [self.store.names[i] for i in obs]
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -181,5 +225,5 @@ class DataParallelEngine:
             h.remove()
         self._hooks = []
         for p in self.store.params:
-            if hasattr(p, "_mg_engine"):
+            if getattr(p, "_mg_engine", None) is self:
                 del p._mg_engine

@@ -84,6 +84,11 @@ def is_initialized() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
+def world_size() -> int:
+    """Ranks in the default process group (1 when none was created)."""
+    return dist.get_world_size() if is_initialized() else 1
+
+
 def barrier():
     if is_initialized():
         dist.barrier()

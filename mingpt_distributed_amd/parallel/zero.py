@@ -1,88 +1,151 @@
-"""ZeRO-1: optimizer state sharded over the data-parallel ranks.
+"""ZeRO-1: optimizer state sharded over the data-parallel ranks, communication overlapped.
 
 SURVEY §2.4 lists FSDP/ZeRO as absent from the reference (its only strategy is DDP,
 ``/root/reference/mingpt/trainer.py:71``) and as the optional next step after replicated DP.
-This is that step, built on the same flat buffers as :class:`DataParallelEngine`:
+This is that step, built on the same flat buffers and bucket layout as
+:class:`DataParallelEngine`:
 
-* The :class:`~mingpt_distributed_amd.optim.FlatParamStore` is padded to ``world * 64``
-  elements, so rank ``r`` owns the contiguous, 16-byte aligned range ``[r*S, (r+1)*S)``.
-* **Gradients**: one ``reduce_scatter_tensor`` of the fp32 main-grad buffer at the step
-  boundary leaves each rank the summed gradient of its own shard (``(N-1)/N`` of the buffer over
-  the links, half of a ring all-reduce's traffic).  It is not overlapped with backward: a single
-  large collective is the bandwidth-optimal shape for point-to-point xGMI rings, and the
-  optimizer needs the whole shard anyway.
-* **Optimizer**: the ``adamw.hip`` kernels run unchanged on the shard slices (chunk table
-  relative to the shard).  The global grad norm is the all-reduced sum of per-shard sums of
-  squares, so clipping matches the replicated optimizer exactly.  Adam moments are allocated
-  for the shard only: ``8 * P / N`` bytes per rank instead of ``8 * P``.
-* **Parameters**: ``all_gather_into_tensor`` of the bf16 compute shard (half the bytes of the
-  fp32 master) rebuilds the full compute weights on every rank.  fp32 master weights outside
-  the shard go stale; :meth:`ZeroAdamW.consolidate` (collective) gathers masters and moments
-  before a snapshot, so checkpoints keep the replicated optimizer's format and load either way.
+* **Layout.**  The :class:`~mingpt_distributed_amd.optim.FlatParamStore` is cut into buckets
+  padded to ``world * 64`` elements; rank ``r`` owns the ``r``-th equal slice of EVERY bucket
+  (interleaved shards), so each bucket's collective is one equal-split reduce-scatter.
+* **Gradients.**  A bucket's ``reduce_scatter_tensor`` launches from inside backward the moment
+  its last gradient lands (same readiness protocol as DP), on RCCL **in place**: the output is
+  the rank's own slice of the input (``out == in + rank * count``), so no gradient shard buffer
+  exists.  ``(N-1)/N`` of the bucket crosses the links: half a ring all-reduce.  With
+  ``reduce_dtype=bf16`` the bucket is converted into a bf16 comm buffer first and the optimizer
+  reads bf16 gradients.
+* **Optimizer.**  The ``adamw.hip`` kernels run on the rank's pieces through a chunk table whose
+  moment offsets are packed (``moment_start``): Adam moments exist for the shard only,
+  ``8 * P / N`` bytes per rank.  The global grad norm is the all-reduced sum of per-shard sums of
+  squares, so clipping equals the replicated optimizer's.
+* **Parameters.**  After the update each bucket's bf16 compute weights are all-gathered in place
+  (input = own slice of the output), asynchronously.  The next forward waits per bucket, right
+  before the first kernel that reads one of its weights (``ops/grads.before_use``): the gather of
+  later layers overlaps the forward of earlier ones.  Forwards that do not go through the fused
+  GPU ops (CPU path, ``no_grad`` inference, generation) wait for everything up front.
+* **Snapshots.**  The fp32 master is replicated in memory, but only the rank's pieces are
+  current: :meth:`ZeroAdamW.consolidate` (collective) all-gathers masters in place (no extra
+  memory) and streams each bucket's moment slices to rank 0, which copies them to host memory.
+  No rank ever holds the full moments on the device; rank 0's host copy is dropped as soon as
+  :meth:`state_dict` has read it.
+* ``world == 1`` runs the same code with the collectives skipped (shard = everything).
 """
 from __future__ import annotations
 
 import math
-from typing import Optional, Set
+from typing import List, Optional, Set
 
 import torch
 import torch.distributed as dist
 
-from ..optim import ALIGN, CHUNK, FlatParamStore, FusedAdamW
-from .ddp import DataParallelEngine
+from ..optim import FlatParamStore, FusedAdamW, make_chunk_table
+from .ddp import DataParallelEngine, _Bucket
 
 
 class ZeroGradEngine(DataParallelEngine):
-    """Gradient side of ZeRO-1: readiness bookkeeping as in DP, one reduce-scatter per step."""
+    """Gradient and parameter side of ZeRO-1 (see module docstring)."""
 
-    def __init__(self, store: FlatParamStore, process_group=None, broadcast: bool = True):
-        super().__init__(store, process_group, bucket_mb=float(store.total * 4) / 2 ** 20 + 1,
-                         broadcast=broadcast)
-        assert store.total % (self.world * ALIGN) == 0, "store must be padded to world * ALIGN"
-        self.rank = dist.get_rank(process_group)
-        self.shard = store.total // self.world
-        self.lo = self.rank * self.shard
-        self.hi = self.lo + self.shard
-        dev = store.device
-        self.grad_shard = torch.zeros(self.shard, dtype=torch.float32, device=dev)
-        self.param_stage = torch.empty(self.shard, dtype=store.flat.dtype, device=dev)
-        # gloo with device tensors (the 2-ranks-on-one-card GPU tests): stage through the list
-        # collectives gloo implements for CUDA; RCCL takes the *_tensor fast path
-        self._gloo_dev = dev.type == "cuda" and dist.get_backend(process_group) == "gloo"
+    def __init__(self, store: FlatParamStore, process_group=None, broadcast: bool = True,
+                 reduce_dtype: Optional[torch.dtype] = None, model: Optional[torch.nn.Module] = None,
+                 comm_at_world1: bool = False):
+        super().__init__(store, process_group, reduce_dtype=reduce_dtype, broadcast=broadcast,
+                         comm_at_world1=comm_at_world1)
+        multi = self.active
+        self.rank = dist.get_rank(process_group) if multi else 0
+        for s, e, _ in store.buckets:
+            if (e - s) % (self.world * 64):
+                raise ValueError("ZeRO-1 needs every bucket padded to world * 64 elements")
+        # this rank's slice of every bucket: (bucket start, end, own lo, own hi)
+        self.own = []
+        for b in self.buckets:
+            sh = (b.end - b.start) // self.world
+            lo = b.start + self.rank * sh
+            self.own.append((lo, lo + sh))
+        self.shard_numel = sum(hi - lo for lo, hi in self.own)
+        self.gather_work: List[Optional[object]] = [None] * len(self.buckets)
+        # gloo (CPU tests, or device tensors staged through the host) has no in-place
+        # reduce-scatter: it all-reduces the whole bucket (2x the traffic, same result)
+        self._gloo = multi and dist.get_backend(process_group) == "gloo"
+        self._hook_handle = None
+        if multi and model is not None:
+            self._hook_handle = model.register_forward_pre_hook(self._forward_pre_hook)
 
-    def _launch_ready(self):
-        return  # no per-bucket collectives: the reduce-scatter runs at the step boundary
+    # ------------------------------------------------------------------ gradients
+    def _launch(self, b: _Bucket):
+        wire = self._wire(b)
+        if self._gloo:
+            b.work = dist.all_reduce(wire, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            return
+        bi = self.buckets.index(b)
+        lo, hi = self.own[bi]
+        out = wire[lo - b.start:hi - b.start]
+        b.work = dist.reduce_scatter_tensor(out, wire, op=dist.ReduceOp.SUM, group=self.pg,
+                                            async_op=True)
 
     def finish(self):
-        if self.world > 1 and self.sync_enabled:
-            if self._gloo_dev:
-                dist.all_reduce(self.store.grad, op=dist.ReduceOp.SUM, group=self.pg)
-                self.grad_shard.copy_(self.store.grad[self.lo:self.hi])
+        self.wait_gathers()  # weights no forward read this step are still owed to the optimizer
+        super().finish()
+
+    def relayout_order(self):
+        self.observed = None  # moments are sharded by layout position: keep the layout
+        return None
+
+    # ------------------------------------------------------------------ parameters
+    def gather_params(self):
+        """Launch the in-place all-gather of every bucket's bf16 compute weights (async)."""
+        if not self.active:
+            return
+        flat = self.store.flat
+        for bi, b in enumerate(self.buckets):
+            lo, hi = self.own[bi]
+            full = flat[b.start:b.end]
+            if self._gloo:
+                shard = flat[lo:hi].clone()
+                self.gather_work[bi] = dist.all_gather(list(full.chunk(self.world)), shard,
+                                                       group=self.pg, async_op=True)
             else:
-                dist.reduce_scatter_tensor(self.grad_shard, self.store.grad, op=dist.ReduceOp.SUM,
-                                           group=self.pg)
-        for b in self.buckets:
-            b.ready = 0
-        self.done = [False] * len(self.done)
-        self.uses = [0] * len(self.uses)
+                self.gather_work[bi] = dist.all_gather_into_tensor(full, flat[lo:hi], group=self.pg,
+                                                                   async_op=True)
 
-    def gather(self, full: torch.Tensor, shard_src: Optional[torch.Tensor] = None):
-        """All-gather rank shards of ``full`` (in place; the local shard is staged first)."""
-        src = full[self.lo:self.hi] if shard_src is None else shard_src
-        stage = self.param_stage if src.dtype == self.param_stage.dtype else src.clone()
-        if stage is self.param_stage:
-            stage.copy_(src)
-        self._all_gather(full, stage)
+    def before_use(self, p):
+        bi = self.bucket_of[self.store.index[id(p)]]
+        w = self.gather_work[bi]
+        if w is not None:
+            w.wait()  # stream-ordered on RCCL: the compute stream waits, the host does not
+            self.gather_work[bi] = None
 
-    def _all_gather(self, full: torch.Tensor, shard: torch.Tensor):
-        if self._gloo_dev:
-            dist.all_gather(list(full.chunk(self.world)), shard, group=self.pg)
-        else:
-            dist.all_gather_into_tensor(full, shard, group=self.pg)
+    def wait_gathers(self):
+        for bi, w in enumerate(self.gather_work):
+            if w is not None:
+                w.wait()
+                self.gather_work[bi] = None
+
+    def _forward_pre_hook(self, module, args):
+        idx = args[0] if args else None
+        if not (isinstance(idx, torch.Tensor) and idx.is_cuda and torch.is_grad_enabled()):
+            self.wait_gathers()
+
+    def all_gather_inplace(self, buf: torch.Tensor):
+        """Synchronously all-gather every bucket of a full-size flat buffer (e.g. fp32 masters)."""
+        if not self.active:
+            return
+        for bi, b in enumerate(self.buckets):
+            lo, hi = self.own[bi]
+            full = buf[b.start:b.end]
+            if self._gloo:
+                dist.all_gather(list(full.chunk(self.world)), buf[lo:hi].clone(), group=self.pg)
+            else:
+                dist.all_gather_into_tensor(full, buf[lo:hi], group=self.pg)
+
+    def close(self):
+        if self._hook_handle is not None:
+            self._hook_handle.remove()
+            self._hook_handle = None
+        super().close()
 
 
 class ZeroAdamW(FusedAdamW):
-    """:class:`FusedAdamW` over this rank's shard of the flat buffers (see module docstring)."""
+    """:class:`FusedAdamW` over this rank's pieces of the flat buffers (see module docstring)."""
 
     def __init__(self, store: FlatParamStore, engine: ZeroGradEngine, lr: float = 3e-4,
                  betas=(0.9, 0.95), eps: float = 1e-8, weight_decay: float = 0.1,
@@ -96,109 +159,147 @@ class ZeroAdamW(FusedAdamW):
         self.wd_of = {n: (weight_decay if n in self.decay_names else 0.0) for n in store.names}
         self.step_count = 0
         dev = store.device
-        lo, hi = engine.lo, engine.hi
-        self.exp_avg = torch.zeros(hi - lo, dtype=torch.float32, device=dev)
-        self.exp_avg_sq = torch.zeros(hi - lo, dtype=torch.float32, device=dev)
+        # packed moment offset of every bucket's own slice
+        self.moff, off = [], 0
+        for lo, hi in engine.own:
+            self.moff.append(off)
+            off += hi - lo
+        self.exp_avg = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(off, dtype=torch.float32, device=dev)
         self.norm_buf = torch.zeros(2, dtype=torch.float32, device=dev)
-        # per-parameter pieces inside the shard (shard-relative), then CHUNK-sized kernel chunks
+        # (global start, end, wd, packed moment start) of every parameter piece this rank owns
         self.pieces = []
-        for name, o, n in zip(store.names, store.offsets, store.numels):
-            a, b = max(o, lo), min(o + n, hi)
-            if a < b:
-                self.pieces.append((a - lo, b - lo, self.wd_of[name]))
-        starts, lens, wds = [], [], []
-        for a, b, wd in self.pieces:
-            for c in range(a, b, CHUNK):
-                starts.append(c)
-                lens.append(min(CHUNK, b - c))
-                wds.append(wd)
-        self.n_chunks = len(starts)
-        self.c_start = torch.tensor(starts, dtype=torch.int64, device=dev)
-        self.c_len = torch.tensor(lens, dtype=torch.int32, device=dev)
-        self.c_wd = torch.tensor(wds, dtype=torch.float32, device=dev)
-        self._full_state = None
+        for (lo, hi), mo in zip(engine.own, self.moff):
+            for a, b, wd in store.pieces(self.wd_of, lo, hi):
+                self.pieces.append((a, b, wd, mo + (a - lo)))
+        self.c_start, self.c_len, self.c_wd, self.c_mstart = make_chunk_table(
+            self.pieces, dev, store.total, off)
+        self.n_chunks = int(self.c_len.numel())
+        self._host_state = None
         self.param_groups = [{"lr": lr, "betas": self.betas, "weight_decay": weight_decay, "eps": eps}]
+
+    @property
+    def grad_buffer(self) -> torch.Tensor:
+        return self.engine.grad_buffer
+
+    @grad_buffer.setter
+    def grad_buffer(self, _v):  # the engine owns it
+        pass
+
+    def _all_reduce_sumsq(self):
+        if self.engine.active:
+            dist.all_reduce(self.norm_buf[:1], group=self.engine.pg)
 
     def step(self, grad_scale: float = 1.0, lr: Optional[float] = None):
         s, e = self.store, self.engine
         lr = self.param_groups[0]["lr"] if lr is None else lr
         self.step_count += 1
-        self._full_state = None
+        self._host_state = None
         b1, b2 = self.betas
-        master, flat, g = s.master[e.lo:e.hi], s.flat[e.lo:e.hi], e.grad_shard
+        g = self.grad_buffer
         if s.device.type == "cuda":
             from ..ops._ext import ext
 
             C = ext()
-            C.grad_sumsq(g, grad_scale, self.norm_buf)  # [0] = local sum of squares (unscaled)
-            dist.all_reduce(self.norm_buf[:1], group=e.pg)
+            C.grad_sumsq_chunks(self.c_start, self.c_len, g, grad_scale, self.norm_buf)
+            self._all_reduce_sumsq()
             torch.mul(self.norm_buf[:1].sqrt(), grad_scale, out=self.norm_buf[1:])
-            if self.n_chunks:
-                C.adamw_step(self.c_start, self.c_len, self.c_wd, master, flat, g, self.exp_avg,
-                             self.exp_avg_sq, self.norm_buf, lr, b1, b2, self.eps, self.step_count,
-                             grad_scale, float(self.grad_clip))
-            e.gather(s.flat)
+            C.adamw_step(self.c_start, self.c_len, self.c_wd, self.c_mstart, s.master, s.flat, g,
+                         self.exp_avg, self.exp_avg_sq, self.norm_buf, lr, b1, b2, self.eps,
+                         self.step_count, grad_scale, float(self.grad_clip))
+            e.gather_params()
             return
-        # CPU path (same math as FusedAdamW's, on the shard)
-        gs = g * grad_scale
-        self.norm_buf[0] = (gs * gs).sum()
-        dist.all_reduce(self.norm_buf[:1], group=e.pg)
+        # CPU path (same math as FusedAdamW's, on the owned pieces)
+        sq = torch.zeros((), dtype=torch.float32)
+        for a, b, _, _ in self.pieces:
+            ga = g[a:b].float() * grad_scale
+            sq += (ga * ga).sum()
+        self.norm_buf[0] = sq
+        self._all_reduce_sumsq()
         self.norm_buf[1] = self.norm_buf[0].sqrt()
+        coef = 1.0
         if self.grad_clip > 0:
-            coef = self.grad_clip / (self.norm_buf[1] + 1e-6)
-            if coef < 1:
-                gs = gs * coef
+            c = self.grad_clip / (self.norm_buf[1].item() + 1e-6)
+            coef = min(1.0, c)
         bc1 = 1 - b1 ** self.step_count
         bc2 = 1 - b2 ** self.step_count
-        self.exp_avg.mul_(b1).add_(gs, alpha=1 - b1)
-        self.exp_avg_sq.mul_(b2).addcmul_(gs, gs, value=1 - b2)
-        for a, b, wd in self.pieces:
+        for a, b, wd, ma in self.pieces:
+            gs = g[a:b].float() * (grad_scale * coef)
+            m = self.exp_avg[ma:ma + b - a]
+            v = self.exp_avg_sq[ma:ma + b - a]
+            m.mul_(b1).add_(gs, alpha=1 - b1)
+            v.mul_(b2).addcmul_(gs, gs, value=1 - b2)
             if wd:
-                master[a:b].mul_(1 - lr * wd)
-            denom = (self.exp_avg_sq[a:b].sqrt() / math.sqrt(bc2)).add_(self.eps)
-            master[a:b].addcdiv_(self.exp_avg[a:b], denom, value=-lr / bc1)
-        if s.flat is not s.master:
-            flat.copy_(master)
-        e.gather(s.flat)
+                s.master[a:b].mul_(1 - lr * wd)
+            denom = (v.sqrt() / math.sqrt(bc2)).add_(self.eps)
+            s.master[a:b].addcdiv_(m, denom, value=-lr / bc1)
+            if s.flat is not s.master:
+                s.flat[a:b].copy_(s.master[a:b])
+        e.gather_params()
+        e.wait_gathers()  # CPU: the next forward reads the weights directly
 
     # ------------------------------------------------------------------ state
     def consolidate(self):
-        """Collective: gather fp32 masters and both moments onto every rank (before a snapshot)."""
+        """Collective.  Every rank: fp32 masters all-gathered in place (no extra memory).  Rank 0:
+        the full Adam moments assembled in HOST memory, one bucket slice at a time (no rank ever
+        holds the full moments on the device)."""
         s, e = self.store, self.engine
-        e.gather(s.master)
-        m = torch.empty(s.total, dtype=torch.float32, device=s.device)
-        v = torch.empty_like(m)
-        e._all_gather(m, self.exp_avg)
-        e._all_gather(v, self.exp_avg_sq)
-        self._full_state = (m, v)
+        e.wait_gathers()
+        e.all_gather_inplace(s.master)
+        is0 = e.rank == 0
+        host = None
+        if is0:
+            host = (torch.zeros(s.total, dtype=torch.float32), torch.zeros(s.total, dtype=torch.float32))
+        for bi, b in enumerate(e.buckets):
+            lo, hi = e.own[bi]
+            sh = hi - lo
+            mo = self.moff[bi]
+            for k, buf in enumerate((self.exp_avg, self.exp_avg_sq)):
+                piece = buf[mo:mo + sh]
+                if not e.active:
+                    host[k][b.start:b.end].copy_(piece)
+                    continue
+                if e._gloo:
+                    piece = piece.cpu()  # gloo gathers host tensors only
+                parts = [torch.empty_like(piece) for _ in range(e.world)] if is0 else None
+                dist.gather(piece, parts, dst=0, group=e.pg)
+                if is0:
+                    host[k][b.start:b.end].copy_(torch.cat(parts))
+        self._host_state = host
 
     def state_dict(self):
-        if self._full_state is None:
-            raise RuntimeError("ZeroAdamW.state_dict: call consolidate() on every rank first")
-        m, v = self._full_state
+        """Replicated-format optimizer state (loads into :class:`FusedAdamW` too).  Needs
+        :meth:`consolidate` first; only rank 0 holds the consolidated moments."""
+        if self._host_state is None:
+            raise RuntimeError("ZeroAdamW.state_dict: call consolidate() on every rank first "
+                               "(the full state is assembled on rank 0 only)")
+        m, v = self._host_state
+        self._host_state = None  # do not keep a host copy of the full moments around
         s = self.store
         st = {}
         for name, o, n, p in zip(s.names, s.offsets, s.numels, s.params):
-            st[name] = {"exp_avg": m[o:o + n].view(p.shape).cpu().clone(),
-                        "exp_avg_sq": v[o:o + n].view(p.shape).cpu().clone(),
+            st[name] = {"exp_avg": m[o:o + n].view(p.shape).clone(),
+                        "exp_avg_sq": v[o:o + n].view(p.shape).clone(),
                         "master": s.master[o:o + n].view(p.shape).cpu().clone()}
         return {"step": self.step_count, "state": st,
                 "hparams": {"lr": self.param_groups[0]["lr"], "betas": list(self.betas), "eps": self.eps,
                             "weight_decay": self.weight_decay, "grad_clip": self.grad_clip}}
 
     def load_state_dict(self, sd):
-        """Every rank loads the full (replicated-format) state and keeps its shard."""
-        s, e = self.store, self.engine
+        """Every rank loads the full (replicated-format) state and keeps its pieces."""
+        s = self.store
         self.step_count = int(sd["step"])
         for name, o, n in zip(s.names, s.offsets, s.numels):
             ent = sd["state"].get(name)
-            if ent is None:
-                continue
-            if "master" in ent:
+            if ent is not None and "master" in ent:
                 s.master[o:o + n].copy_(ent["master"].reshape(-1))
-            a, b = max(o, e.lo), min(o + n, e.hi)
-            if a < b:
-                self.exp_avg[a - e.lo:b - e.lo].copy_(ent["exp_avg"].reshape(-1)[a - o:b - o])
-                self.exp_avg_sq[a - e.lo:b - e.lo].copy_(ent["exp_avg_sq"].reshape(-1)[a - o:b - o])
+        for a, b, _, ma in self.pieces:
+            for name, o, n in zip(s.names, s.offsets, s.numels):
+                if o <= a and b <= o + n:
+                    ent = sd["state"].get(name)
+                    if ent is not None:
+                        self.exp_avg[ma:ma + b - a].copy_(ent["exp_avg"].reshape(-1)[a - o:b - o])
+                        self.exp_avg_sq[ma:ma + b - a].copy_(ent["exp_avg_sq"].reshape(-1)[a - o:b - o])
+                    break
         s.sync_params_from_master()
-        self._full_state = None
+        self._host_state = None

@@ -53,7 +53,10 @@ class StepEngine:
     def __init__(self, model: torch.nn.Module, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
                  weight_decay: float = 0.1, grad_clip: float = 1.0, decay_names=None,
                  device: Optional[torch.device] = None, bucket_mb: float = 32.0, reduce_dtype=None,
-                 zero1: bool = False):
+                 zero1: bool = False, comm_at_world1: bool = False):
+        """``reduce_dtype``: None (fp32 gradients on the wire) or ``torch.bfloat16``.
+        ``zero1``: shard the AdamW state over the data-parallel ranks (also valid at world 1).
+        ``comm_at_world1``: drive the collectives even in a one-rank process group (tests)."""
         if device is None:
             info = D.info()
             if info.device.type == "cuda":
@@ -63,33 +66,68 @@ class StepEngine:
             else:
                 device = torch.device("cpu")
         self.device = torch.device(device)
+        if self.device.type == "cuda" and hasattr(getattr(model, "config", None), "check_gpu_support"):
+            model.config.check_gpu_support()  # fail at construction, not inside the first step
         self.model = model.to(self.device)
         if decay_names is None:
             decay_names, _ = param_groups(model)
-        multi = D.is_initialized() and torch.distributed.get_world_size() > 1
-        self.zero1 = bool(zero1 and multi)
-        okw = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, decay_names=decay_names,
-                   grad_clip=grad_clip or 0.0)
+        multi = D.is_initialized() and (torch.distributed.get_world_size() > 1 or comm_at_world1)
+        world = torch.distributed.get_world_size() if multi else 1
+        self.comm_at_world1 = comm_at_world1
+        if reduce_dtype == "auto":
+            reduce_dtype = None
+        self.zero1 = bool(zero1)
+        self._okw = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, decay_names=decay_names,
+                         grad_clip=grad_clip or 0.0)
+        self.bucket_mb, self.reduce_dtype = bucket_mb, reduce_dtype
+        bucket_numel = DataParallelEngine.bucket_numel(bucket_mb) if (multi or zero1) else None
         if self.zero1:  # optimizer state sharded over the ranks (parallel/zero.py)
             from .parallel.zero import ZeroAdamW, ZeroGradEngine
 
-            self.store = FlatParamStore(model, device=self.device,
-                                        pad_multiple=64 * torch.distributed.get_world_size())
-            self.dp = ZeroGradEngine(self.store)
-            self.opt = ZeroAdamW(self.store, self.dp, **okw)
+            self.store = FlatParamStore(model, device=self.device, bucket_numel=bucket_numel,
+                                        bucket_align=64 * world)
+            self.dp = ZeroGradEngine(self.store, reduce_dtype=reduce_dtype, model=model,
+                                     comm_at_world1=comm_at_world1)
+            self.opt = ZeroAdamW(self.store, self.dp, **self._okw)
         else:
-            self.store = FlatParamStore(model, device=self.device)
-            self.opt = FusedAdamW(self.store, **okw)
-            self.dp = DataParallelEngine(self.store, bucket_mb=bucket_mb, reduce_dtype=reduce_dtype) \
-                if multi else None
+            self.store = FlatParamStore(model, device=self.device, bucket_numel=bucket_numel)
+            self.opt = FusedAdamW(self.store, **self._okw)
+            self.dp = DataParallelEngine(self.store, bucket_mb=bucket_mb, reduce_dtype=reduce_dtype,
+                                         comm_at_world1=comm_at_world1) if multi else None
+            if self.dp is not None:
+                self.opt.grad_buffer = self.dp.grad_buffer
         self.world = self.dp.world if self.dp else 1
         self._hooks = []
         self.annotate = False  # record_function ranges (fwd/bwd/allreduce/optim) while profiling
-        if self.dp is None:
+        self._fold_hooks()
+
+    def _fold_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        if self.dp is None or not self.dp.active:
             # single process: ops that return ordinary autograd grads (the CPU reference path)
             # are folded into the fp32 main-grad buffer the optimizer reads
             for p in self.store.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(_fold_grad))
+
+    def _relayout(self, order):
+        """Rebuild the flat buffers (and so the all-reduce buckets) in ``order`` -- the gradient
+        completion order the data-parallel engine observed in the first backward -- keeping
+        fp32 masters and Adam moments (DDP's bucket rebuild after iteration 1)."""
+        old_store, old_dp = self.store, self.dp
+        old_dp.close()
+        new = FlatParamStore(self.model, device=self.device,
+                             bucket_numel=DataParallelEngine.bucket_numel(self.bucket_mb),
+                             order=order, master_from=old_store)
+        self.opt.rehome(new)
+        self.store = new
+        self.dp = DataParallelEngine(new, bucket_mb=self.bucket_mb, reduce_dtype=self.reduce_dtype,
+                                     broadcast=False, comm_at_world1=self.comm_at_world1)
+        self.dp.observed = None
+        self.dp._recording = None
+        self.opt.grad_buffer = self.dp.grad_buffer
+        self._graph = None
 
     @classmethod
     def from_torch_optimizer(cls, model, optimizer: torch.optim.Optimizer, grad_clip: float, **kw):
@@ -139,6 +177,10 @@ class StepEngine:
         with self._range("mingpt::optimizer"):
             self.opt.step(grad_scale=1.0 / self.world)
             self.store.zero_grad()
+        if self.dp is not None:
+            order = self.dp.relayout_order()
+            if order is not None:
+                self._relayout(order)
 
     def train_step(self, batches) -> torch.Tensor:
         """One optimizer step over a list of (x, y) micro-batches; returns the mean loss (device)."""

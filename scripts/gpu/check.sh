@@ -19,7 +19,7 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 if [ $TESTS = 1 ]; then
-  timeout -k 10 600 python -m pytest tests/ -m gpu -q -p no:cacheprovider -x > "$OUT/tests.log" 2>&1
+  timeout -k 10 900 python -u -m pytest tests/ -m gpu -q -p no:cacheprovider -x --timeout 300 --timeout-method thread > "$OUT/tests.log" 2>&1
   s=$?; tail -3 "$OUT/tests.log"; [ $s -eq 0 ] || exit $s
 fi
 timeout -k 10 400 python bench.py $BARGS > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 1; }

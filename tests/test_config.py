@@ -1,4 +1,5 @@
 """Config system: presets (XOR semantics, reference D8), aliases (D14), YAML + overrides, CfgNode."""
+import os
 import pytest
 
 from mingpt_distributed_amd.models.config import GPTConfig, PRESETS
@@ -76,3 +77,18 @@ def test_zero1_override_reaches_trainer_config():
 
     assert load_run_config(None, ["trainer_config.zero1=true"]).trainer_config.zero1 is True
     assert load_run_config(None, []).trainer_config.zero1 is False
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """`bench.py --gpus N` without a torchrun env launches N ranks itself, and fails loudly (never
+    a silent 1-GPU number labelled N) when fewer GPUs are visible -- here, on CPU, zero are."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "--gpus 2 requested but only 0 GPU(s) are visible" in r.stderr

@@ -39,14 +39,16 @@ def _batch():
     return torch.randint(0, 50, (4, 16), generator=g), torch.randint(0, 50, (4, 16), generator=g)
 
 
-def _worker_dp(rank, world, port, out_dir, accum):
+def _worker_dp(rank, world, port, out_dir, accum, bf16=False):
     _init(rank, world, port)
     import torch.distributed as dist
 
     from mingpt_distributed_amd.trainer import StepEngine
 
-    eng = StepEngine(_model(), lr=1e-2, grad_clip=1.0, bucket_mb=0.01)  # tiny buckets: many collectives
+    eng = StepEngine(_model(), lr=1e-2, grad_clip=1.0, bucket_mb=0.01,  # tiny buckets: many collectives
+                     reduce_dtype=torch.bfloat16 if bf16 else None)
     assert eng.dp is not None and len(eng.dp.buckets) > 3
+    assert (eng.dp.comm is not None) == bf16
     x, y = _batch()
     per = x.shape[0] // world
     xs, ys = x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per]
@@ -61,13 +63,13 @@ def _worker_dp(rank, world, port, out_dir, accum):
     dist.all_gather(gathered, flat)
     assert torch.equal(gathered[0], gathered[1]), "ranks diverged"
     if rank == 0:
-        torch.save(flat, os.path.join(out_dir, f"dp_{accum}.pt"))
+        torch.save(eng.model_state_dict(), os.path.join(out_dir, f"dp_{accum}.pt"))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("accum", [False, True])
-def test_dp_matches_single_process(tmp_path, accum):
-    mp.spawn(_worker_dp, args=(2, _port(), str(tmp_path), accum), nprocs=2, join=True)
+@pytest.mark.parametrize("accum,bf16", [(False, False), (True, False), (False, True)])
+def test_dp_matches_single_process(tmp_path, accum, bf16):
+    mp.spawn(_worker_dp, args=(2, _port(), str(tmp_path), accum, bf16), nprocs=2, join=True)
     from mingpt_distributed_amd.trainer import StepEngine
 
     eng = StepEngine(_model(), lr=1e-2, grad_clip=1.0, device=torch.device("cpu"))
@@ -75,8 +77,77 @@ def test_dp_matches_single_process(tmp_path, accum):
     for _ in range(3):
         eng.train_step([(x, y)])
     dp = torch.load(tmp_path / f"dp_{accum}.pt", weights_only=True)
-    # summation order differs (gloo sum of half-batch grads); Adam amplifies it only on ~0 grads
-    torch.testing.assert_close(dp, eng.store.master, atol=1e-4, rtol=1e-4)
+    for k, v in eng.model_state_dict().items():
+        if bf16:
+            # bf16 gradients on the wire (8 mantissa bits): Adam normalises the update, so weights
+            # move by ~lr per step either way; a flipped sign on a ~0 gradient costs <= 2 lr
+            assert (dp[k] - v).abs().max().item() <= 3 * 2e-2, k
+            assert torch.nn.functional.cosine_similarity(dp[k].flatten() - _init_of(k),
+                                                         v.flatten() - _init_of(k), dim=0) > 0.95, k
+        else:
+            # summation order differs (gloo sum of half-batch grads); Adam amplifies it only on ~0 grads
+            torch.testing.assert_close(dp[k], v, atol=1e-4, rtol=1e-4)
+
+
+def _init_of(name):
+    return _model().state_dict()[name].detach().float().flatten()
+
+
+class _Crossed(torch.nn.Module):
+    """Registration order a, b, c but forward uses c first: the layout's reverse registration
+    order (a's bucket last) is not the order gradients complete in (a's gradient first)."""
+
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.a = torch.nn.Linear(16, 16)
+        self.b = torch.nn.Linear(16, 16)
+        self.c = torch.nn.Linear(16, 16)
+
+    def forward(self, x, y):
+        h = self.a(torch.tanh(self.b(torch.tanh(self.c(x)))))
+        return h, ((h - y) ** 2).mean()
+
+
+def _worker_relayout(rank, world, port, out_dir):
+    _init(rank, world, port)
+    from mingpt_distributed_amd.trainer import StepEngine
+
+    eng = StepEngine(_Crossed(), lr=1e-2, grad_clip=1.0, bucket_mb=0.0005, decay_names=set())
+    before = list(eng.store.names)
+    g = torch.Generator().manual_seed(rank)
+    x, y = torch.randn(8, 16, generator=g), torch.randn(8, 16, generator=g)
+    eng.train_step([(x, y)])
+    after = list(eng.store.names)
+    assert after != before and after[:2] == ["a.bias", "a.weight"] or after[:2] == ["a.weight", "a.bias"], after
+    # buckets now follow the observed order: the first bucket holds only a's parameters
+    first = [eng.store.names[i] for i in eng.store.buckets[0][2]]
+    assert all(n.startswith("a.") for n in first), first
+    for _ in range(2):
+        eng.train_step([(x, y)])
+    if rank == 0:
+        torch.save(eng.model_state_dict(), os.path.join(out_dir, "relayout.pt"))
+    import torch.distributed as dist
+
+    dist.destroy_process_group()
+
+
+def test_dp_rebuilds_buckets_in_observed_order(tmp_path):
+    mp.spawn(_worker_relayout, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+    from mingpt_distributed_amd.trainer import StepEngine
+
+    eng = StepEngine(_Crossed(), lr=1e-2, grad_clip=1.0, device=torch.device("cpu"), decay_names=set())
+    xs, ys = [], []
+    for r in range(2):
+        g = torch.Generator().manual_seed(r)
+        xs.append(torch.randn(8, 16, generator=g))
+        ys.append(torch.randn(8, 16, generator=g))
+    x, y = torch.cat(xs), torch.cat(ys)
+    for _ in range(3):
+        eng.train_step([(x, y)])
+    got = torch.load(tmp_path / "relayout.pt", weights_only=True)
+    for k, v in eng.model_state_dict().items():
+        torch.testing.assert_close(got[k], v, atol=1e-5, rtol=1e-5)
 
 
 def _worker_trainer(rank, world, port, out_dir):

@@ -150,9 +150,52 @@ def test_adamw_matches_torch():
         opt.step()
         C.grad_sumsq(g, 1.0, norm)
         torch.testing.assert_close(norm[1], total, rtol=1e-4, atol=1e-4)
-        C.adamw_step(cs, cl, cw, master, param, g, m, v, norm, 1e-3, 0.9, 0.95, 1e-8, step, 1.0, 1.0)
+        C.adamw_step(cs, cl, cw, None, master, param, g, m, v, norm, 1e-3, 0.9, 0.95, 1e-8, step, 1.0, 1.0)
     torch.testing.assert_close(master, torch.cat([p.detach() for p in ref_params]), atol=1e-5, rtol=1e-4)
     _close(param, master, atol=1e-2)
+
+
+@pytest.mark.parametrize("gdtype", [torch.float32, torch.bfloat16])
+def test_adamw_pieces_packed_moments(gdtype):
+    """The ZeRO-1 form: the kernels update only some pieces of the flat buffers (a rank's slice of
+    every bucket), the moments are packed (moment_start), the gradients may be the bf16 buffer a
+    bf16 reduction left; grad_sumsq_chunks covers exactly those pieces.  Oracle: plain fp32 math."""
+    from mingpt_distributed_amd.optim import make_chunk_table
+
+    C = ext()
+    torch.manual_seed(0)
+    n = 200_000
+    pieces = [(0, 40_000, 0.1, 0), (70_016, 140_032, 0.0, 40_000), (150_016, 199_936, 0.1, 110_016)]
+    nm = sum(b - a for a, b, _, _ in pieces)
+    cs, cl, cw, cm = make_chunk_table(pieces, DEV, n, nm)
+    master = torch.randn(n, device=DEV)
+    param = master.to(torch.bfloat16)
+    g = torch.randn(n, device=DEV).to(gdtype)
+    m = torch.zeros(nm, device=DEV)
+    v = torch.zeros(nm, device=DEV)
+    ref_master, ref_m, ref_v = master.clone(), m.clone(), v.clone()
+    norm = torch.zeros(2, device=DEV)
+    lr, b1, b2, eps, gs, clip = 1e-3, 0.9, 0.95, 1e-8, 0.5, 1.0
+    for step in range(1, 3):
+        C.grad_sumsq_chunks(cs, cl, g, gs, norm)
+        gf = g.float()
+        sq = sum((gf[a:b] * gs).pow(2).sum() for a, b, _, _ in pieces)
+        torch.testing.assert_close(norm[1], sq.sqrt(), rtol=1e-4, atol=1e-4)
+        C.adamw_step(cs, cl, cw, cm, master, param, g, m, v, norm, lr, b1, b2, eps, step, gs, clip)
+        coef = min(1.0, clip / (sq.sqrt().item() + 1e-6))
+        for a, b, wd, ma in pieces:
+            gg = gf[a:b] * gs * coef
+            mm, vv = ref_m[ma:ma + b - a], ref_v[ma:ma + b - a]
+            mm.mul_(b1).add_(gg, alpha=1 - b1)
+            vv.mul_(b2).addcmul_(gg, gg, value=1 - b2)
+            ref_master[a:b].mul_(1 - lr * wd)
+            denom = vv.sqrt() / (1 - b2 ** step) ** 0.5 + eps
+            ref_master[a:b].addcdiv_(mm, denom, value=-lr / (1 - b1 ** step))
+    torch.testing.assert_close(master, ref_master, atol=1e-5, rtol=1e-4)  # untouched outside pieces
+    torch.testing.assert_close(m, ref_m, atol=1e-6, rtol=1e-4)
+    torch.testing.assert_close(v, ref_v, atol=1e-7, rtol=1e-4)
+    with pytest.raises(ValueError):
+        make_chunk_table([(0, n + 64, 0.0, None)], DEV, n)
 
 
 @pytest.mark.parametrize("N", [768, 2304, 3072, 520])  # 32- and 64-lane bias-grad row chunks

@@ -134,3 +134,15 @@ def test_from_pretrained_synthetic_hf():
     g1 = m.generate(x[:1, :4], 8, do_sample=False)
     g2 = hf.generate(x[:1, :4], max_new_tokens=8, do_sample=False, pad_token_id=0)
     assert torch.equal(g1, g2)
+
+
+def test_gpu_shape_validation_is_early():
+    """GPU-unsupported shapes are rejected on the host, before any kernel launch."""
+    from mingpt_distributed_amd.models import GPTConfig
+
+    assert GPTConfig(model_type="gpt2").resolve().gpu_unsupported() is None
+    assert GPTConfig(model_type="gpt2-xl").resolve().gpu_unsupported() is None
+    bad = GPTConfig(n_layer=1, n_head=3, n_embed=60).resolve()  # head dim 20, n_embed % 8 != 0
+    assert "multiple of 8" in bad.gpu_unsupported()
+    with pytest.raises(ValueError, match="not supported by the GPU kernels"):
+        bad.check_gpu_support()

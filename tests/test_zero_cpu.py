@@ -18,8 +18,9 @@ def _worker_zero(rank, world, port, out_dir, accum):
     from mingpt_distributed_amd.parallel.zero import ZeroAdamW
     from mingpt_distributed_amd.trainer import StepEngine
 
-    eng = StepEngine(_model(), lr=1e-2, grad_clip=1.0, zero1=True)
+    eng = StepEngine(_model(), lr=1e-2, grad_clip=1.0, zero1=True, bucket_mb=0.01)
     assert eng.zero1 and isinstance(eng.opt, ZeroAdamW)
+    assert len(eng.dp.buckets) > 3  # one reduce-scatter / all-gather per bucket
     assert eng.opt.exp_avg.numel() * world == eng.store.total
     x, y = _batch()
     per = x.shape[0] // world
@@ -36,10 +37,15 @@ def _worker_zero(rank, world, port, out_dir, accum):
     dist.all_gather(gathered, flat)
     for g in gathered[1:]:
         assert torch.equal(gathered[0], g), "ranks diverged"
-    sd = eng.opt.state_dict()
     if rank == 0:
-        torch.save({"master": flat, "opt": sd, "norm": eng.grad_norm.clone()},
+        sd = eng.opt.state_dict()
+        with pytest.raises(RuntimeError):  # the host copy is dropped once read
+            eng.opt.state_dict()
+        torch.save({"model": eng.model_state_dict(), "opt": sd, "norm": eng.grad_norm.clone()},
                    os.path.join(out_dir, f"zero_{accum}.pt"))
+    else:
+        with pytest.raises(RuntimeError):  # only rank 0 assembles the full state
+            eng.opt.state_dict()
     dist.destroy_process_group()
 
 
@@ -53,8 +59,9 @@ def test_zero1_matches_single_process(tmp_path, world, accum):
     for _ in range(3):
         eng.train_step([(x, y)])
     z = torch.load(tmp_path / f"zero_{accum}.pt", weights_only=True)
-    n = eng.store.total
-    torch.testing.assert_close(z["master"][:n], eng.store.master, atol=1e-4, rtol=1e-4)
+    ref_sd = eng.model_state_dict()
+    for k, v in ref_sd.items():  # by name: the ZeRO layout pads every bucket
+        torch.testing.assert_close(z["model"][k], v, atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(z["norm"], eng.grad_norm, atol=1e-4, rtol=1e-4)
     # the consolidated ZeRO state loads into the replicated optimizer and matches its moments
     ref = eng.opt.state_dict()
@@ -79,7 +86,7 @@ def _worker_resume(rank, world, port, out_dir):
     eng.train_step([(x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per])])
     eng.opt.consolidate()
     if rank == 0:
-        torch.save(eng.store.master.clone(), os.path.join(out_dir, "resumed.pt"))
+        torch.save(eng.model_state_dict(), os.path.join(out_dir, "resumed.pt"))
     dist.destroy_process_group()
 
 
@@ -94,7 +101,8 @@ def test_zero1_resumes_from_replicated_snapshot(tmp_path):
     eng.train_step([(x, y)])
     mp.spawn(_worker_resume, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
     resumed = torch.load(tmp_path / "resumed.pt", weights_only=True)
-    torch.testing.assert_close(resumed[:eng.store.total], eng.store.master, atol=1e-4, rtol=1e-4)
+    for k, v in eng.model_state_dict().items():
+        torch.testing.assert_close(resumed[k], v, atol=1e-4, rtol=1e-4)
 
 
 def _worker_trainer_zero(rank, world, port, out_dir):
