@@ -44,9 +44,6 @@ def main():
         out, lse, mask = C.attention_fwd(qkv, B, T, H, p, 1)
         tf = timeit(lambda: C.attention_fwd(qkv, B, T, H, p, 1))
         tb = timeit(lambda: C.attention_bwd(qkv, out, dout, lse, mask, B, T, H, p, 1))
-        C.attention_set_bwd_variant(1)
-        tb128 = timeit(lambda: C.attention_bwd(qkv, out, dout, lse, mask, B, T, H, p, 1))
-        C.attention_set_bwd_variant(0)
         q, k, v = qkv.view(B, T, 3, H, hd).permute(2, 0, 3, 1, 4).unbind(0)
         q, k, v = (t.contiguous().requires_grad_() for t in (q, k, v))
         go = dout.view(B, T, H, hd).transpose(1, 2).contiguous()
@@ -57,7 +54,7 @@ def main():
             o = F.scaled_dot_product_attention(q, k, v, dropout_p=p, is_causal=True)
             torch.autograd.grad(o, (q, k, v), go)
         sfb = timeit(sdpa_bwd)
-        print(json.dumps({"p": p, "mine_fwd_ms": round(tf, 3), "mine_bwd_ms": round(tb, 3), "mine_bwd128_ms": round(tb128, 3),
+        print(json.dumps({"p": p, "mine_fwd_ms": round(tf, 3), "mine_bwd_ms": round(tb, 3),
                           "sdpa_fwd_ms": round(sf, 3), "sdpa_fwd+bwd_ms": round(sfb, 3),
                           "mine_fwd_tflops": round(flops_fwd / tf / 1e9, 1),
                           "mine_bwd_tflops": round(2.5 * flops_fwd / tb / 1e9, 1)}), flush=True)

@@ -378,7 +378,7 @@ std::vector<at::Tensor> attention_fwd(const at::Tensor& qkv, int64_t B, int64_t 
   CHECK_BF16(qkv); CHECK_CONTIG(qkv);
   const int64_t D3 = qkv.size(-1), D = D3 / 3, hd = D / H;
   TORCH_CHECK(D3 == 3 * D && D == H * hd && qkv.numel() == B * T * D3, "attention: qkv shape");
-  TORCH_CHECK(hd % 8 == 0 && hd <= 64, "attention: head dim must be a multiple of 8 and <= 64");
+  TORCH_CHECK(hd % 8 == 0 && hd <= 128, "attention: head dim must be a multiple of 8 and <= 128");
   DevGuard g(qkv.device());
   auto out = at::empty({B * T, D}, qkv.options());
   auto lse = at::empty({B * H * T}, qkv.options().dtype(at::kFloat));
@@ -398,13 +398,14 @@ at::Tensor attention_bwd(const at::Tensor& qkv, const at::Tensor& out, const at:
   CHECK_CONTIG(qkv); CHECK_CONTIG(out); CHECK_CONTIG(dout);
   const int64_t D3 = qkv.size(-1), D = D3 / 3, hd = D / H;
   TORCH_CHECK(qkv.numel() == B * T * D3 && out.numel() == B * T * D && dout.numel() == B * T * D &&
-              lse.numel() == B * H * T && hd % 8 == 0 && hd <= 64, "attention_bwd: shape mismatch");
-  TORCH_CHECK((hd & (hd - 1)) == 0, "attention_bwd: head dim must be a power of two (8..64)");
+              lse.numel() == B * H * T && hd % 8 == 0 && hd <= 128, "attention_bwd: shape mismatch");
+  TORCH_CHECK(B * T * H * 16 < (int64_t)1 << 31, "attention_bwd: B*T*H too large");
   DevGuard g(qkv.device());
   auto dqkv = at::empty_like(qkv);
   auto opts = qkv.options().dtype(at::kFloat);
   auto delta = at::empty({B * H * T}, opts);
-  auto dq = at::empty({mg::attention_bwd_keyblocks((int)T) * B * T * D}, opts);  // dQ partials
+  // fp32 dQ accumulator (persistent mode) or per-key-block partials (attention_train.hip)
+  auto dq = at::empty({(int64_t)mg::attention_bwd_workspace_floats((int)B, (int)T, (int)H, (int)hd)}, opts);
   const uint32_t* mp = nullptr;
   if (p > 0) {
     CHECK_DEV(mask);
@@ -497,7 +498,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_bwd", &gelu_bwd);
   m.def("dropout_bwd", &dropout_bwd);
   m.def("transpose", &transpose);
-  m.def("attention_set_bwd_variant", &mg::attention_set_bwd_variant);
   m.def("bias_grad", &bias_grad);
   m.def("dropout_bias_grad", &dropout_bias_grad);
   m.def("gemm", &gemm, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("layout"), py::arg("epi"),
@@ -505,6 +505,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("N"), py::arg("dbias") = py::none());
   m.def("gemm_set_variant", &mg::gemm_set_variant);
   m.def("gemm_get_variant", &mg::gemm_get_variant);
+  m.def("attention_set_bwd_mode", &mg::attention_set_bwd_mode);
   m.def("attention_fwd", &attention_fwd);
   m.def("attention_bwd", &attention_bwd);
   m.def("gemv", &gemv, py::arg("x"), py::arg("W"), py::arg("epi"), py::arg("bias") = py::none(),

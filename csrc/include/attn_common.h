@@ -1,0 +1,87 @@
+// Shared pieces of the attention kernels (attention.hip: decode; attention_train.hip: training
+// forward / backward and the dropout keep-bit generator).
+#pragma once
+#include "common.h"
+
+namespace mg {
+namespace attn {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// LDS images hold 64 head-dim columns per row (128 B); a head dim > 64 is stored as two such
+// 64-column halves, each its own [rows][128 B] image, so every fragment read below is the same.
+constexpr int ROWB = 128;
+constexpr float kNegBig = -1e30f;
+
+// conflict-free for ds_read_b128 (32-row operand) and both ds_read_b64_tr_b16 patterns
+MG_DEVICE int swz(int r) { return ((r >> 1) & 3) | ((((r >> 1) ^ (r >> 3)) & 1) << 2); }
+MG_DEVICE int lds_off(int row, int ch) { return row * ROWB + ((ch ^ swz(row)) << 4); }
+// byte offset of a transposed-read lane address (row, column) in an lds_off image
+MG_DEVICE int tr_off(int row, int col) { return lds_off(row, col >> 3) + (col & 7) * 2; }
+
+struct AttnArgs {
+  const bf16_t* qkv;
+  bf16_t* out;
+  float* lse;          // [B*H*T], log2 domain of the scaled scores
+  const bf16_t* dout;  // bwd
+  const float* delta;  // bwd [B*H*T]
+  float* dq;           // bwd fp32 dQ accumulator [B*T, D] (or per-key-block partials)
+  long dq_part;        // bwd partial mode: elements between the per-key-block dQ partials (0: persistent)
+  bf16_t* dqkv;        // bwd [B*T, 3D]
+  const uint32_t* dmask;  // dropout keep-bits, layout: attention_train.hip (mask kernel)
+  int B, T, H, hd, D;
+  float scale_log2;    // log2(e) / sqrt(hd)
+  uint32_t thr;        // 8-bit keep threshold: keep iff random byte >= thr (0 = no dropout)
+  float dscale;        // 1 / (1 - thr/256)
+};
+
+MG_DEVICE float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }  // v_exp_f32, no denorm fixup
+
+// 32-bit avalanche mixer (xorshift-multiply, "lowbias32" constants): a bijection with good
+// avalanche; the attention-dropout bytes are mix32 of distinct counters.
+MG_DEVICE uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+inline uint32_t mix32_host(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+
+MG_DEVICE bf16x8 lds_row_at(const char* base, int o) { return *reinterpret_cast<const bf16x8*>(base + o); }
+
+// Transposed fragment from two per-lane offsets (rows r0+q and r0+8+q, or +4): the swizzle is
+// periodic in the row with period 16, so a 16-row-aligned row base is a plain byte offset the
+// caller passes as a compile-time constant (it lands in the ds_read offset field).
+MG_DEVICE bf16x8 lds_tr_at(const char* base, int oa, int ob) {
+  const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + oa));
+  const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + ob));
+  const s16x8 v = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// 8 consecutive accumulator values -> one bf16x8 MFMA operand (4 v_cvt_pk_bf16_f32)
+MG_DEVICE bf16x8 pack_frag(const f32x16& a, int s) {
+  const uint4 u = make_uint4(pack2(a[8 * s], a[8 * s + 1]), pack2(a[8 * s + 2], a[8 * s + 3]),
+                             pack2(a[8 * s + 4], a[8 * s + 5]), pack2(a[8 * s + 6], a[8 * s + 7]));
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+// combine a value with the partner lane's (lane ^ 32) on gfx950: one v_permlane32_swap leaves
+// {low-half value, high-half value} in the two results on every lane, no per-lane select
+MG_DEVICE float max_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+MG_DEVICE float sum_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+}  // namespace attn
+}  // namespace mg

@@ -80,15 +80,16 @@ void gemm_set_variant(int v);  // tile config override: 0 auto (per shape), 1..5
 void gemm_set_debug_buffer(unsigned long long* p);  // MG_GEMM_STAMPS diagnostic builds
 int gemm_get_variant();
 
-// attention.hip -- causal flash attention, hd <= 64; qkv [B*T, 3D], out [B*T, D], lse [B*H*T]
-// dmask: dropout keep-bits written by fwd when p > 0 (attention_dropout_mask_words u32), read by bwd
+// attention_train.hip / attention.hip -- causal flash attention; qkv [B*T, 3D], out [B*T, D],
+// lse [B*H*T]; dmask: dropout keep-bits generated by attention_fwd when p > 0
+// (attention_dropout_mask_words u32), read by attention_bwd
 size_t attention_dropout_mask_words(int B, int T, int H);
-void attention_set_bwd_variant(int v);  // 0 auto (256-key blocks), 1 force 128-key blocks
 void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, uint32_t* dmask, int B, int T, int H,
                    int hd, float p, uint64_t seed, hipStream_t stream);
-// delta [B*H*T] and dq [attention_bwd_keyblocks(T) * B*T*D] fp32 are workspaces; writes all three
+// delta [B*H*T] and dq [attention_bwd_workspace_floats] fp32 are workspaces; writes all three
 // slots of dqkv
-int attention_bwd_keyblocks(int T);
+size_t attention_bwd_workspace_floats(int B, int T, int H, int hd);
+void attention_set_bwd_mode(int mode);  // 0 auto, 1 persistent (b, h) workgroups, 2 key-block partials
 void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse,
                    const uint32_t* dmask, float* delta, float* dq, bf16_t* dqkv, int B, int T, int H,
                    int hd, float p, uint64_t seed, hipStream_t stream);

@@ -1,0 +1,855 @@
+// Causal flash attention for training on gfx950 (CDNA4, MI355X): dropout keep-bit generator,
+// forward and backward.  (Decode: attention.hip.)
+//
+// Replaces the reference's nn.MultiheadAttention math path
+// (/root/reference/mingpt/model.py:147-165: in-proj split, q*scale, baddbmm with the [T,T] mask,
+// softmax, dropout, bmm PV, plus the discarded head-averaged weights) with a true causal kernel
+// that never materialises [T, T] (fixes D4: the reference's additive 0/1 mask was not causal).
+//
+// Head dims: any multiple of 8 up to 128.  The kernels are instantiated per number of 16-column
+// MFMA k-steps (NKS = ceil(hd / 16) rounded to {1, 2, 3, 4, 6, 8}); columns past hd are zero in
+// the LDS images and the Q fragments, so they add nothing.  LDS images hold 64 columns per row;
+// hd > 64 uses two 64-column halves (attn_common.h).
+//
+// Dropout on the attention probabilities (the reference's MHA dropout, model.py:150): the keep
+// bits are generated up front by attn_dropmask_kernel -- one u32 per (b, h, 64-key tile half,
+// query) -- and read by both passes, so the forward's inner loop carries no hashing (at hd = 64
+// the forward is VALU-bound: the hash was ~40 % of its vector instructions).
+//
+// Forward (FA2 structure, MI355X mapping):
+//  * workgroup = 4 waves = 128 queries of one (b, h); each wave owns 32 queries.
+//  * Q fragments live in VGPRs for the whole kernel, pre-multiplied by log2(e)/sqrt(hd): S comes
+//    out of the MFMA in the log2 domain and p = exp2(S - m) costs one subtract per score.
+//  * K/V tiles of 64 keys are staged through LDS (double buffer; tile t+1's global loads are in
+//    flight during tile t's MFMAs; per-thread addresses are computed once).
+//  * S^T = K Q^T with v_mfma_f32_32x32x16_bf16 ("swapped" operands): the query is on the lane, so
+//    the softmax row statistics are lane-local; the two 32-key halves of a row meet through one
+//    v_permlane32_swap (max) and the row sum is combined only once, after the last tile.
+//  * the online-softmax rescale is lazy: a row's running max moves only when a score exceeds it
+//    by more than 8 (log2 units; p <= 256 in between), which after the first tile is rare.
+//  * P is converted to bf16 in registers and used directly as the B operand of O^T = V^T P^T;
+//    V^T fragments come from LDS with ds_read_b64_tr_b16 in the matching permuted key order.
+//  * heaviest (last) query blocks are launched first; fully-masked K tiles are skipped per wave.
+#include "attn_common.h"
+#include "kernels.h"
+
+using namespace mg;
+using namespace mg::attn;
+
+namespace {
+
+// ------------------------------------------------------------------------------- dropout bits
+// word (bh, j, q), j = 2 * tile + h, covers the 32 scores one forward lane holds for query q in
+// 64-key tile `tile`, half h: value e = 16 * sub + r  <->  key
+//   64 * tile + 32 * sub + 4 * h + (r & 3) + 8 * (r >> 2),
+// at bit drop_bit(e) = 8 (e & 3) + (e >> 2) (the SWAR order below: no bit gathering; both
+// passes test a compile-time / per-lane constant bit).  Stored [bh][j][q]: lanes of consecutive
+// queries read consecutive words in both passes.  keep iff random byte >= thr.
+// Randomness: one lowbias32 mix of the word index and seed, then xorshift32 steps -- shifts and
+// xors only (32-bit integer multiplies are quarter rate; 26 of them per word made this kernel
+// cost half the forward).
+__global__ __launch_bounds__(256) void attn_dropmask_kernel(uint32_t* __restrict__ dmask, int BH, int T,
+                                                            int ntw, uint64_t seed,
+                                                            const uint64_t* __restrict__ sofs,
+                                                            uint32_t thr) {
+  // grid (BH, ceil(T / 256)); a thread makes every word its query needs: the tiles up to its
+  // diagonal (j = 0 .. 2 * (q / 64) + 1).  One word per thread launched ~100k workgroups and
+  // cost 4x its arithmetic; 32-bit index math (64-bit div/mod cost more than the hashing).
+  const int bh = blockIdx.x;
+  const int q = blockIdx.y * 256 + threadIdx.x;
+  if (q >= T) return;
+  const uint64_t sd = eff_seed(seed, sofs);
+  const uint32_t key = (uint32_t)sd ^ mix32((uint32_t)(sd >> 32) + 0x9E3779B9u);
+  const uint32_t kadd = (thr <= 128 ? 128u - thr : 256u - thr) * 0x01010101u;
+  const int jend = min(ntw, 2 * (q / 64) + 2);
+  uint32_t* out = dmask + (long)bh * ntw * T + q;
+  for (int j = 0; j < jend; ++j) {
+    const uint32_t i = (uint32_t)((bh * ntw + j) * T + q);  // the word's index (wraps past 2^32: fine)
+    uint32_t x = mix32(i ^ key) | 1u;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      x ^= x << 13;
+      x ^= x >> 17;
+      x ^= x << 5;
+      // SWAR: bit 7 of byte b <- (byte >= thr); value e = 4 w + b lands at bit 8 b + w
+      const uint32_t y = (x & 0x7f7f7f7fu) + kadd;
+      const uint32_t k7 = (thr <= 128 ? (y | x) : (y & x)) & 0x80808080u;
+      bits |= k7 >> (7 - w);
+    }
+    out[(long)j * T] = bits;
+  }
+}
+
+// ------------------------------------------------------------------------------- forward
+// sign-extended bit e of w (0 or -1): one v_bfe_i32 (the builtin was lowered to and+cmp+select)
+template <int E>
+MG_DEVICE int keep_bit(uint32_t w) {
+  int r;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(r) : "v"(w), "n"(E));
+  return r;
+}
+
+template <int E>
+MG_DEVICE void drop_at(f32x16 (&s)[2], uint32_t kw) {
+  constexpr int BIT = 8 * (E & 3) + (E >> 2);  // attn_dropmask_kernel's bit of value E
+  s[E >> 4][E & 15] = __int_as_float(__float_as_int(s[E >> 4][E & 15]) & keep_bit<BIT>(kw));
+  if constexpr (E + 1 < 32) drop_at<E + 1>(s, kw);
+}
+
+// One 64-key tile for one wave's 32 queries: S^T = K Q^T, online softmax, O^T += V^T P^T.
+template <int NKS, bool MASK>
+MG_DEVICE void fwd_tile(const AttnArgs& a, const char* sk, const char* sv, const int (&ko)[NKS],
+                        const bf16x8 (&qf)[NKS], f32x16 (&o)[(NKS + 1) / 2], float& m, float& l,
+                        uint32_t kw, int lim, int ta0, int tb0, int ta1, int tb1) {
+  constexpr int NO = (NKS + 1) / 2;
+  constexpr int HALF = 64 * ROWB;
+  f32x16 s[2];
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub) {
+    s[sub] = f32x16{0};
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+      s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_at(sk + sub * 32 * ROWB, ko[ks]), qf[ks],
+                                                       s[sub], 0, 0, 0);
+  }
+  if constexpr (MASK) {  // key = k0 + c(sub, r) + 4 h32, c a constant: one compare per score
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        s[sub][r] = (sub * 32 + (r & 3) + 8 * (r >> 2) > lim) ? kNegBig : s[sub][r];
+  }
+  float mx = s[0][0];
+#pragma unroll
+  for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s[0][r]);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[1][r]);
+  mx = max_xor32(mx);
+  // lazy rescale: move a row's max only when a score exceeds it by more than 2^8
+  const bool grow = mx > m + 8.f;
+  if (__any(grow)) {
+    const float mn = grow ? mx : m;
+    const float alpha = fexp2(m - mn);
+    m = mn;
+    l *= alpha;
+#pragma unroll
+    for (int n = 0; n < NO; ++n) o[n] *= alpha;
+  }
+  float rs = 0.f;
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = fexp2(s[sub][r] - m);
+      rs += p;
+      s[sub][r] = p;
+    }
+  l += rs;
+  // dropout for O only (l sums the undropped P); the keep scale is applied to O at the end
+  drop_at<0>(s, kw);
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const bf16x8 pf = pack_frag(s[sub], st);
+      const int rb = (sub * 32 + 16 * st) * ROWB;  // 16-row aligned: an immediate
+#pragma unroll
+      for (int n = 0; n < NO; ++n) {
+        const char* vb = sv + (n >> 1) * HALF + rb;
+        o[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            (n & 1) ? lds_tr_at(vb, ta1, tb1) : lds_tr_at(vb, ta0, tb0), pf, o[n], 0, 0, 0);
+      }
+    }
+}
+
+template <int NKS>  // 16-column k-steps covering the head dim
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
+  constexpr int NH = (NKS + 3) / 4;   // 64-column halves of the LDS images
+  constexpr int NO = (NKS + 1) / 2;   // 32-column O^T accumulator tiles
+  constexpr int HALF = 64 * ROWB;     // one 64-row, 64-column image
+  constexpr int TILE = NH * HALF;     // one K or V tile
+  constexpr int NC = 2 * NH;          // 16-byte chunks per thread per tile per matrix
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // K0 V0 K1 V1
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h32 = lane >> 5, l32 = lane & 31;
+  const int nqb = (a.T + 127) / 128;
+  const int bh = blockIdx.x % (a.B * a.H);
+  const int qb = nqb - 1 - blockIdx.x / (a.B * a.H);  // heaviest blocks first
+  const int b = bh / a.H, hh = bh % a.H;
+  const int q0 = qb * 128;
+  const long ld = 3L * a.D;
+  const bf16_t* Qg = a.qkv + (long)b * a.T * ld + hh * a.hd;
+  const bf16_t* Kg = Qg + a.D;
+  const bf16_t* Vg = Qg + 2 * a.D;
+  const int myq = q0 + 32 * w + l32;
+
+  // Q fragments (k-step ks: columns 16 ks + 8 h32 .. +7), scaled into the log2 domain
+  bf16x8 qf[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    const int d = ks * 16 + 8 * h32;
+    uint4 u = (myq < a.T && d < a.hd) ? ld16(Qg + (long)myq * ld + d) : make_uint4(0, 0, 0, 0);
+    float f[8];
+    unpack8(u, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] *= a.scale_log2;
+    qf[ks] = __builtin_bit_cast(bf16x8, pack8(f));
+  }
+
+  // tile staging: chunk c of this thread -> (half, row, 16-byte column chunk); offsets once
+  int srow[NC], scol[NC], sdst[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int idx = threadIdx.x + 256 * c;
+    const int hf = idx >> 9, rem = idx & 511;
+    srow[c] = rem >> 3;
+    scol[c] = hf * 64 + (rem & 7) * 8;
+    sdst[c] = hf * HALF + lds_off(rem >> 3, rem & 7);
+  }
+  auto load_tile = [&](uint4 (&rk)[NC], uint4 (&rv)[NC], int k0) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int r = k0 + srow[c];
+      const bool ok = r < a.T && scol[c] < a.hd;
+      const long go = (long)r * ld + scol[c];
+      rk[c] = ok ? ld16(Kg + go) : make_uint4(0, 0, 0, 0);
+      rv[c] = ok ? ld16(Vg + go) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_tile = [&](char* dst, const uint4 (&rk)[NC], const uint4 (&rv)[NC]) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      *reinterpret_cast<uint4*>(dst + sdst[c]) = rk[c];
+      *reinterpret_cast<uint4*>(dst + TILE + sdst[c]) = rv[c];
+    }
+  };
+
+  // per-lane fragment offsets: K rows l32 (+32 per sub: an immediate), chunk 2 ks + h32;
+  // V^T transposed reads rows 4 h32 + q (+8), columns (n & 1) * 32 + cb + 4 p
+  int ko[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) ko[ks] = (ks >> 2) * HALF + lds_off(l32, (2 * ks + h32) & 7);
+  const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+  const int ta0 = tr_off(4 * h32 + trq, trc), tb0 = tr_off(8 + 4 * h32 + trq, trc);
+  const int ta1 = tr_off(4 * h32 + trq, 32 + trc), tb1 = tr_off(8 + 4 * h32 + trq, 32 + trc);
+
+  f32x16 o[NO];
+#pragma unroll
+  for (int n = 0; n < NO; ++n) o[n] = f32x16{0};
+  float m = kNegBig, l = 0.f;
+  const int kend = min(a.T, q0 + 128);
+  const int ntiles = (kend + 63) / 64;
+  const int wave_qmax = q0 + 32 * w + 31;
+  const int ntw = 2 * ((a.T + 63) / 64);
+  const uint32_t* mrow = a.dmask + (long)bh * ntw * a.T + myq;  // word (bh, j, myq) at mrow[j * T]
+
+  {
+    uint4 rk[NC], rv[NC];
+    load_tile(rk, rv, 0);
+    store_tile(smem, rk, rv);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const char* sk = smem + (t & 1) * 2 * TILE;
+    const char* sv = sk + TILE;
+    const bool more = t + 1 < ntiles;
+    uint4 rk[NC], rv[NC];
+    if (more) load_tile(rk, rv, (t + 1) * 64);
+    const int k0 = t * 64;
+    if (k0 <= wave_qmax) {
+      // keep bits of this lane's 32 scores (issued first: latency hidden by the S MFMAs)
+      const uint32_t kw = (a.thr && myq < a.T) ? mrow[(long)(2 * t + h32) * a.T] : 0xffffffffu;
+      // the causal / sequence-end mask only on the tiles that need it: two copies of the body,
+      // so the common path carries no per-score compare (a uniform branch inside one body got
+      // if-converted into 32 compares + selects on every tile)
+      if (k0 + 63 > q0 + 32 * w || k0 + 64 > a.T)
+        fwd_tile<NKS, true>(a, sk, sv, ko, qf, o, m, l, kw, min(myq, a.T - 1) - k0 - 4 * h32, ta0, tb0, ta1, tb1);
+      else
+        fwd_tile<NKS, false>(a, sk, sv, ko, qf, o, m, l, kw, 0, ta0, tb0, ta1, tb1);
+    }
+    if (more) store_tile(smem + ((t + 1) & 1) * 2 * TILE, rk, rv);
+    __syncthreads();
+  }
+
+  l = sum_xor32(l);
+  if (myq < a.T) {
+    const float inv = (a.thr ? a.dscale : 1.f) / l;
+    if (h32 == 0) a.lse[(long)bh * a.T + myq] = m + log2f(l);  // log2 domain
+    bf16_t* orow = a.out + ((long)b * a.T + myq) * a.D + hh * a.hd;
+#pragma unroll
+    for (int n = 0; n < NO; ++n)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = n * 32 + 8 * g + 4 * h32;
+        if (d < a.hd)
+          *reinterpret_cast<uint2*>(orow + d) = make_uint2(pack2(o[n][4 * g] * inv, o[n][4 * g + 1] * inv),
+                                                           pack2(o[n][4 * g + 2] * inv, o[n][4 * g + 3] * inv));
+      }
+  }
+}
+
+// =============================================================================== backward
+// delta[(b*H + h)*T + t] = sum_d dO * O.  One lane per 16-byte chunk (8 elements) of a head row,
+// lanes of consecutive chunks/heads/tokens read contiguous memory; the ceil(hd/8) lanes of a
+// head row are reduced with xor-shuffles (groups padded to a power of two).
+__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restrict__ dout,
+                                                           const bf16_t* __restrict__ out,
+                                                           float* __restrict__ delta, int BT, int T,
+                                                           int H, int hd, int lg) {
+  // thread -> (row bt, head h, chunk c < cpr = 2^lg): cpr = chunks per head row rounded up to a
+  // power of two; 32-bit index arithmetic (B*T*H*cpr < 2^31 is checked on the host)
+  const int cpr = 1 << lg;
+  const unsigned i = blockIdx.x * 256u + threadIdx.x;
+  const int c = (int)(i & (cpr - 1));
+  const unsigned rh = i >> lg;
+  const int hh = (int)(rh % (unsigned)H);
+  const int bt = (int)(rh / (unsigned)H);
+  float s = 0.f;
+  if (bt < BT && c * 8 < hd) {
+    const long e = bt * H * hd + (long)hh * hd + c * 8;
+    float x[8], y[8];
+    unpack8(ld16(dout + e), x);
+    unpack8(ld16(out + e), y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += x[j] * y[j];
+  }
+  for (int o = 1; o < cpr; o <<= 1) s += __shfl_xor(s, o, 64);
+  if (bt < BT && c == 0) {
+    const int t = (int)(bt % T), b = (int)(bt / T);
+    delta[((long)b * H + hh) * T + t] = s;
+  }
+}
+
+constexpr int BQ = 64;  // queries per backward tile
+
+// In place on one 32x32 (query rows x key lanes) tile: s <- dropped P (dV operand), dp <- dS.
+// K is pre-scaled by c in LDS, so S' = Q (cK)^T - lse arrives in the log2 domain and p = exp2(S').
+// Dropout keeps/zeroes with a sign-extended bit field and its 1/(1-p) is folded into dS through
+// one FMA and into dV at the store: dS = P * (Z dP~ / (1-p) - delta); s <- Z P.
+template <bool MASK>
+MG_DEVICE void bwd_softmax_grad(f32x16& s, f32x16& dp, const float (&dl)[16], const uint32_t (&mwr)[16],
+                                float dscale, int T, int mykey, int mw_bit, int q0) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float p = fexp2(s[r]);
+    if constexpr (MASK) {
+      const int q = q0 + (r & 3) + 8 * (r >> 2);
+      const bool kill = (mykey > q) | (q >= T);  // bitwise: no short-circuit branches
+      p = kill ? 0.f : p;
+    }
+    // no dropout: every keep word is all ones (set when staged), dscale = 1
+    const int keep = __builtin_amdgcn_sbfe((int)mwr[r], mw_bit, 1);  // 0 or -1
+    s[r] = __int_as_float(__float_as_int(p) & keep);
+    const float dpv = __int_as_float(__float_as_int(dp[r]) & keep);
+    dp[r] = p * __builtin_fmaf(dpv, dscale, -dl[r]);
+  }
+}
+
+// Staging of a [ROWS][NH * 64] bf16 tile (columns >= hd zero) into NH 64-column LDS images.
+// Addresses are recomputed from threadIdx at each use (a few VALU ops): holding them across the
+// kernel cost the backward its last free registers.
+template <int ROWS, int NH, int NT>
+struct Stager {
+  static constexpr int N = ROWS * 8 * NH / NT;  // 16-byte chunks per thread
+  static MG_DEVICE void load(uint4 (&reg)[N], const bf16_t* base, long ld, int r0, int rows, int hd) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) {
+      const int idx = threadIdx.x + NT * c;
+      const int rem = idx % (ROWS * 8);
+      const int r = r0 + (rem >> 3), col = (idx / (ROWS * 8)) * 64 + (rem & 7) * 8;
+      reg[c] = (r < rows && col < hd) ? ld16(base + (long)r * ld + col) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  static MG_DEVICE void store(char* lds, const uint4 (&reg)[N]) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) {
+      const int idx = threadIdx.x + NT * c;
+      const int rem = idx % (ROWS * 8);
+      *reinterpret_cast<uint4*>(lds + (idx / (ROWS * 8)) * ROWS * ROWB + lds_off(rem >> 3, rem & 7)) = reg[c];
+    }
+  }
+};
+
+// Key-block-parallel backward, one workgroup per (b, h) sweeping its key blocks in order.
+//  * KW waves = KB = 32 KW keys per block (K pre-scaled by log2(e)/sqrt(hd), and V, in LDS);
+//    each wave keeps dK^T / dV^T accumulators (keys on the lane) across the block's query sweep.
+//  * per 64-query tile (Q, dO, lse, delta, keep-words staged in LDS, the next tile prefetched in
+//    VGPRs): S and dP with the key on the lane, P and dS in registers feed dV^T += dO^T P and
+//    dK^T += Q^T dS directly (transposed reads of Q / dO); dS^T goes through LDS once for
+//    dQ = dS K (the waves split the 32x32 dQ tiles and, where there are more waves than tiles,
+//    the keys; partial tiles meet in LDS).
+//  * dQ of a query tile is summed over the key blocks in a fp32 buffer that only this workgroup
+//    touches (the first block stores, later ones read-add-store; each element always by the
+//    same lane, so program order is the only ordering needed) and written as bf16 into dqkv by
+//    the last block that reaches the tile: no per-key-block partial buffers, no finalize pass.
+//  * attention dropout: the forward's keep bits (attn_dropmask_kernel), one word per query and
+//    32-key half tile, staged 64 queries x KW words per tile.
+template <int NKS, int KW>
+__global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) {
+  constexpr int NH = (NKS + 3) / 4, NO = (NKS + 1) / 2;
+  constexpr int NT = 64 * KW, KB = 32 * KW;
+  constexpr int HQ = BQ * ROWB, HK = KB * ROWB;  // one 64-column half of a Q / K image
+  constexpr int TILES = 2 * NO;                  // 32x32 dQ tiles of a 64-query tile
+  constexpr int KSPLIT = KW >= TILES ? KW / TILES : 1;
+  constexpr int OFF_Q = 0, OFF_DO = OFF_Q + NH * HQ, OFF_K = OFF_DO + NH * HQ;
+  constexpr int OFF_V = OFF_K + NH * HK, OFF_DS = OFF_V + NH * HK, OFF_L = OFF_DS + KB * ROWB;
+  constexpr int OFF_MW = OFF_L + 2 * BQ * 4, OFF_P = OFF_MW + KW * BQ * 4;
+  constexpr int OFF_PV = OFF_P + (KSPLIT > 1 ? (KSPLIT - 1) * TILES * 64 * 16 * 4 : 0);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int w = threadIdx.x >> 6;
+  const int BH = a.B * a.H;
+  const int bh = blockIdx.x % BH;
+  const int b = bh / a.H, hh = bh % a.H;
+  const long ld = 3L * a.D;
+  const bf16_t* Qg = a.qkv + (long)b * a.T * ld + hh * a.hd;
+  const bf16_t* Kg = Qg + a.D;
+  const bf16_t* Vg = Qg + 2 * a.D;
+  const bf16_t* dOg = a.dout + (long)b * a.T * a.D + hh * a.hd;
+  const float* lseg = a.lse + (long)bh * a.T;
+  const float* dlg = a.delta + (long)bh * a.T;
+  char* sK = smem + OFF_K;
+  char* sV = smem + OFF_V;
+  char* sdS = smem + OFF_DS;
+  const float* sL = reinterpret_cast<const float*>(smem + OFF_L);
+  const uint32_t* sMW = reinterpret_cast<const uint32_t*>(smem + OFF_MW);
+  const int ntw = 2 * ((a.T + 63) / 64);
+  const int nqt = (a.T + BQ - 1) / BQ;
+  const int nkb = (a.T + KB - 1) / KB;
+  const float dq_scale = 0.6931471805599453f;  // dQ = dS (c K) ln 2 = dS K / sqrt(hd)
+
+  using stq = Stager<BQ, NH, NT>;
+  using stk = Stager<KB, NH, NT>;
+
+  // this wave's dQ tiles: (tile, key split); tiles are (q-subtile qs, 32-column block n)
+  const int my_split = KSPLIT > 1 ? w / TILES : 0;
+  constexpr int KSPAN = KB / KSPLIT;  // keys per split (a multiple of 16)
+  constexpr int NTW = KSPLIT > 1 ? 1 : (TILES + KW - 1) / KW;  // dQ tiles per wave
+  const int tt0 = KSPLIT > 1 ? w % TILES : w;
+  constexpr int TSTEP = KSPLIT > 1 ? TILES : KW;
+
+  // persistent mode (dq_part == 0): this workgroup sweeps every key block of its (b, h); partial
+  // mode: workgroup = one key block (heaviest first), its dQ contribution stored as partial kb
+  const bool part = a.dq_part != 0;
+  const int kb_lo = part ? blockIdx.x / BH : 0, kb_hi = part ? kb_lo + 1 : nkb;
+  for (int kb = kb_lo; kb < kb_hi; ++kb) {
+    const int kb0 = kb * KB;
+    int mykey, wave_kmin;
+    {
+      const int lane = threadIdx.x & 63, h32 = lane >> 5, l32 = lane & 31;
+      mykey = kb0 + 32 * w + l32;
+      wave_kmin = kb0 + 32 * w;
+      uint4 rk[Stager<KB, NH, NT>::N];
+      stk::load(rk, Kg, ld, kb0, a.T, a.hd);
+#pragma unroll
+      for (int i = 0; i < Stager<KB, NH, NT>::N; ++i) {  // K <- c K (see bwd_softmax_grad)
+        float f[8];
+        unpack8(rk[i], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] *= a.scale_log2;
+        rk[i] = pack8(f);
+      }
+      uint4 rv[stk::N];
+      stk::load(rv, Vg, ld, kb0, a.T, a.hd);
+      __syncthreads();  // the previous block's readers of sK / sV are done
+      stk::store(sK, rk);
+      stk::store(sV, rv);
+      (void)h32; (void)l32;
+    }
+    // this lane's dropout bit inside the keep words (attn_dropmask_kernel layout)
+    const int mw_col = (w >> 1) * 2 + ((mykey >> 2) & 1);
+    const int mw_el = ((mykey & 32) >> 1) | (mykey & 3) | (((mykey >> 3) & 3) << 2);
+    const int mw_bit = 8 * (mw_el & 3) + (mw_el >> 2);
+    const int t0w = (kb0 / 64) * 2;
+
+    f32x16 dk[NO], dv[NO];
+#pragma unroll
+    for (int n = 0; n < NO; ++n) {
+      dk[n] = f32x16{0};
+      dv[n] = f32x16{0};
+    }
+    const int qt0 = kb0 / BQ;
+
+    uint4 rq[Stager<BQ, NH, NT>::N], rd[Stager<BQ, NH, NT>::N];
+    float rl = 0.f;
+    uint32_t rmw = 0xffffffffu;  // no dropout: every key kept
+    auto issue = [&](int qt) {
+      stq::load(rq, Qg, ld, qt * BQ, a.T, a.hd);
+      stq::load(rd, dOg, a.D, qt * BQ, a.T, a.hd);
+      const int t = threadIdx.x;
+      if (t < 2 * BQ) {
+        const int q = qt * BQ + (t & (BQ - 1));
+        rl = q < a.T ? (t < BQ ? -lseg[q] : dlg[q]) : 0.f;  // -lse: the S init (K holds c K)
+      }
+      if (a.thr) {  // word j of query row q -> sMW[j * 64 + q]
+        const int q = qt * BQ + (t & 63), j = t >> 6;
+        rmw = (q < a.T && t0w + j < ntw) ? a.dmask[((long)bh * ntw + t0w + j) * a.T + q] : 0u;
+      }
+    };
+    auto commit = [&]() {
+      stq::store(smem + OFF_Q, rq);
+      stq::store(smem + OFF_DO, rd);
+      if (threadIdx.x < 2 * BQ) reinterpret_cast<float*>(smem + OFF_L)[threadIdx.x] = rl;
+      reinterpret_cast<uint32_t*>(smem + OFF_MW)[threadIdx.x] = rmw;
+    };
+    issue(qt0);
+    commit();
+    __syncthreads();
+
+    for (int qt = qt0; qt < nqt; ++qt) {
+      const char* sQ = smem + OFF_Q;
+      const char* sdO = smem + OFF_DO;
+      int lane = threadIdx.x & 63;
+      asm volatile("" : "+v"(lane));  // recomputed per tile: keeps the offsets below out of the loop state
+      const int h32 = lane >> 5, l32 = lane & 31;
+      const bool more = qt + 1 < nqt;
+      const int qbase = qt * BQ;
+      // dQ bookkeeping of this tile: first key block stores, later ones read-add-store, the last
+      // one to reach the tile writes bf16
+      const int last_kb = min(nkb - 1, (qbase + BQ - 1) / KB);
+      const bool first = part || kb == 0, last = !part && kb == last_kb;
+      if (more) issue(qt + 1);
+      // previous key blocks' dQ sums of this wave's tiles: LDS-DMA'd now (no registers held),
+      // added after the dQ MFMAs (a load in the store loop exposed a memory latency per tile)
+      float* pvs = reinterpret_cast<float*>(smem + OFF_PV) + (my_split == 0 ? w : 0) * NTW * 16 * 64;
+      if (!first && my_split == 0) {
+#pragma unroll
+        for (int i = 0; i < NTW; ++i) {
+          const int tt = tt0 + i * TSTEP;
+          if (tt < TILES) {
+            const int qs = tt / NO, n = tt % NO;
+            const int q0 = qbase + qs * 32 + 4 * h32;
+            const int d = min(n * 32 + l32, a.hd - 1);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int q = min(q0 + (r & 3) + 8 * (r >> 2), a.T - 1);  // rows past T: unused
+              __builtin_amdgcn_global_load_lds(a.dq + ((long)b * a.T + q) * a.D + hh * a.hd + d,
+                                               (__attribute__((address_space(3))) void*)(pvs + (i * 16 + r) * 64),
+                                               4, 0, 0);
+            }
+          }
+        }
+      }
+      char* myds = sdS + w * 32 * ROWB;
+      int ro[NKS], rk_[NKS];
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        ro[ks] = (ks >> 2) * HQ + lds_off(l32, (2 * ks + h32) & 7);
+        rk_[ks] = (ks >> 2) * HK + 32 * w * ROWB + lds_off(l32, (2 * ks + h32) & 7);
+      }
+      const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+      const int ta0 = tr_off(4 * h32 + trq, trc), tb0 = tr_off(8 + 4 * h32 + trq, trc);
+      const int ta1 = tr_off(4 * h32 + trq, 32 + trc), tb1 = tr_off(8 + 4 * h32 + trq, 32 + trc);
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        const int qsub0 = qbase + qs * 32;
+        if (qsub0 + 31 < wave_kmin || wave_kmin >= a.T) {  // every query precedes every key: dS = 0
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int qc = qs * 32 + 8 * g + 4 * h32;
+            *reinterpret_cast<uint2*>(myds + lds_off(l32, qc >> 3) + (qc & 7) * 2) = make_uint2(0, 0);
+          }
+          continue;
+        }
+        float dl[16];
+        uint32_t mwr[16];
+        f32x16 sacc, dp = {0};
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {  // row constants of this lane's 16 rows, 4 per ds_read_b128
+          const int q4 = qs * 32 + 8 * g + 4 * h32;
+          const float4 x = *reinterpret_cast<const float4*>(sL + q4);
+          const float4 y = *reinterpret_cast<const float4*>(sL + BQ + q4);
+          sacc[4 * g] = x.x; sacc[4 * g + 1] = x.y; sacc[4 * g + 2] = x.z; sacc[4 * g + 3] = x.w;
+          dl[4 * g] = y.x; dl[4 * g + 1] = y.y; dl[4 * g + 2] = y.z; dl[4 * g + 3] = y.w;
+          const uint4 m4 = *reinterpret_cast<const uint4*>(sMW + mw_col * 64 + q4);
+          mwr[4 * g] = m4.x; mwr[4 * g + 1] = m4.y; mwr[4 * g + 2] = m4.z; mwr[4 * g + 3] = m4.w;
+        }
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {  // S' = Q (cK)^T - lse ; dP~ = dO V^T
+          sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_at(sQ + qs * 32 * ROWB, ro[ks]),
+                                                         lds_row_at(sK, rk_[ks]), sacc, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_at(sdO + qs * 32 * ROWB, ro[ks]),
+                                                       lds_row_at(sV, rk_[ks]), dp, 0, 0, 0);
+        }
+        // wave-uniform: only diagonal / past-T tiles pay for the causal mask
+        if (wave_kmin + 31 > qsub0 || qsub0 + 31 >= a.T)
+          bwd_softmax_grad<true>(sacc, dp, dl, mwr, a.dscale, a.T, mykey, mw_bit, qsub0 + 4 * h32);
+        else
+          bwd_softmax_grad<false>(sacc, dp, dl, mwr, a.dscale, a.T, mykey, mw_bit, qsub0 + 4 * h32);
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const bf16x8 pf = pack_frag(sacc, st);
+          const bf16x8 dsf = pack_frag(dp, st);
+          const int rb = (qs * 32 + 16 * st) * ROWB;  // 16-row aligned: an immediate
+#pragma unroll
+          for (int n = 0; n < NO; ++n) {
+            const int hb = (n >> 1) * HQ + rb;
+            const bool odd = n & 1;
+            dv[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                odd ? lds_tr_at(sdO + hb, ta1, tb1) : lds_tr_at(sdO + hb, ta0, tb0), pf, dv[n], 0, 0, 0);
+            dk[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                odd ? lds_tr_at(sQ + hb, ta1, tb1) : lds_tr_at(sQ + hb, ta0, tb0), dsf, dk[n], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {  // dS^T image row = key, 4 consecutive q per 8-byte write
+          const int qc = qs * 32 + 8 * g + 4 * h32;
+          *reinterpret_cast<uint2*>(myds + lds_off(l32, qc >> 3) + (qc & 7) * 2) =
+              make_uint2(pack2(dp[4 * g], dp[4 * g + 1]), pack2(dp[4 * g + 2], dp[4 * g + 3]));
+        }
+      }
+      __syncthreads();  // dS of all KB keys in LDS
+      // dQ[64 q][hd] = dS[64 q][KB keys] (c K)[KB keys][hd]
+#pragma unroll
+      for (int i = 0; i < NTW; ++i) {
+        const int tt = tt0 + i * TSTEP;
+        if (tt >= TILES) break;
+        const int qs = tt / NO, n = tt % NO;
+        const int klo = my_split * KSPAN;
+        const bool act = n * 32 < a.hd && qbase + qs * 32 + 31 >= kb0 + klo && kb0 + klo < a.T;
+        f32x16 dq = {0};
+        if (act) {
+          // rows klo + 16 kk + 8 h32 + q (+4): the 16 kk part is an immediate
+          const int da = tr_off(8 * h32 + trq, qs * 32 + trc), db = tr_off(8 * h32 + 4 + trq, qs * 32 + trc);
+          const int ka = tr_off(8 * h32 + trq, (n & 1) * 32 + trc), kb4 = tr_off(8 * h32 + 4 + trq, (n & 1) * 32 + trc);
+          const char* sdSh = sdS + klo * ROWB;
+          const char* sKh = sK + (n >> 1) * HK + klo * ROWB;
+#pragma unroll
+          for (int kk = 0; kk < KSPAN / 16; ++kk)
+            dq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_at(sdSh + kk * 16 * ROWB, da, db),
+                                                         lds_tr_at(sKh + kk * 16 * ROWB, ka, kb4), dq, 0, 0, 0);
+        }
+        if constexpr (KSPLIT > 1) {  // key splits 1.. hand their partial tile to split 0 via LDS
+          float* part = reinterpret_cast<float*>(smem + OFF_P);
+          if (my_split > 0) {
+            float* pp = part + (((my_split - 1) * TILES + tt) * 64 + lane) * 16;
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              *reinterpret_cast<f32x4*>(pp + 4 * g) = f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
+          }
+          __syncthreads();
+          if (my_split == 0) {
+#pragma unroll
+            for (int sp = 1; sp < KSPLIT; ++sp) {
+              const float* pp = part + (((sp - 1) * TILES + tt) * 64 + lane) * 16;
+#pragma unroll
+              for (int g = 0; g < 4; ++g) {
+                const f32x4 x = *reinterpret_cast<const f32x4*>(pp + 4 * g);
+                dq[4 * g] += x[0]; dq[4 * g + 1] += x[1]; dq[4 * g + 2] += x[2]; dq[4 * g + 3] += x[3];
+              }
+            }
+          }
+        }
+        const int d = n * 32 + l32;
+        if (my_split == 0 && d < a.hd && qbase + qs * 32 + 31 >= kb0) {
+          if (!first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
+          // row q0 + (r & 3) + 8 (r >> 2): one 64-bit base per lane, then uniform row strides
+          const int q0 = qbase + qs * 32 + 4 * h32;
+          const long roff = ((long)b * a.T + q0) * a.D + hh * a.hd + d;
+          float* dqb = a.dq + (part ? kb * a.dq_part : 0) + roff;
+          bf16_t* outq = a.dqkv + ((long)b * a.T + q0) * ld + hh * a.hd + d;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int dr = (r & 3) + 8 * (r >> 2);
+            if (q0 + dr < a.T) {
+              const float v = first ? dq[r] : dq[r] + pvs[(i * 16 + r) * 64 + lane];
+              if (last)
+                outq[(long)dr * ld] = f2bf(v * dq_scale);
+              else
+                dqb[(long)dr * a.D] = v;
+            }
+          }
+        }
+      }
+      if (more) commit();
+      __syncthreads();
+    }
+
+    // dK (scaled), dV (dropout keep scale folded) -> dqkv K / V slots; lane = key,
+    // d = n*32 + 8*(r>>2) + 4*h32 + (r&3)
+    const int lane = threadIdx.x & 63, h32 = lane >> 5;
+    if (mykey < a.T) {
+      const float sc = a.scale_log2 * 0.6931471805599453f;  // 1/sqrt(hd)
+      const float vs = a.thr ? a.dscale : 1.f;
+      bf16_t* krow = a.dqkv + ((long)b * a.T + mykey) * ld + a.D + hh * a.hd;
+      bf16_t* vrow = krow + a.D;
+#pragma unroll
+      for (int n = 0; n < NO; ++n)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = n * 32 + 8 * g + 4 * h32;
+          if (d < a.hd) {
+            *reinterpret_cast<uint2*>(krow + d) = make_uint2(pack2(dk[n][4 * g] * sc, dk[n][4 * g + 1] * sc),
+                                                             pack2(dk[n][4 * g + 2] * sc, dk[n][4 * g + 3] * sc));
+            *reinterpret_cast<uint2*>(vrow + d) = make_uint2(pack2(dv[n][4 * g] * vs, dv[n][4 * g + 1] * vs),
+                                                             pack2(dv[n][4 * g + 2] * vs, dv[n][4 * g + 3] * vs));
+          }
+        }
+    }
+  }
+}
+
+// partial mode: dqkv Q slot = bf16(scale * sum of the dQ partials of key blocks kb <= t / KB)
+__global__ __launch_bounds__(256) void attn_dq_finalize_kernel(const float* __restrict__ dq,
+                                                               bf16_t* __restrict__ dqkv, int rows,
+                                                               int D, int T, int KB, long part, float sc) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;  // over rows * D/8
+  const int d8 = D / 8;
+  if (i >= (long)rows * d8) return;
+  const int r = (int)(i / d8);  // 32-bit operands: a cheap division
+  const int c = (int)(i - (long)r * d8) * 8;
+  const int np = (r % T) / KB + 1;
+  float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
+  for (int k = 0; k < np; ++k) {
+    const float* src = dq + k * part + (long)r * D + c;
+    const float4 y0 = *reinterpret_cast<const float4*>(src), y1 = *reinterpret_cast<const float4*>(src + 4);
+    x0.x += y0.x; x0.y += y0.y; x0.z += y0.z; x0.w += y0.w;
+    x1.x += y1.x; x1.y += y1.y; x1.z += y1.z; x1.w += y1.w;
+  }
+  const float f[8] = {x0.x * sc, x0.y * sc, x0.z * sc, x0.w * sc, x1.x * sc, x1.y * sc, x1.z * sc, x1.w * sc};
+  st16(dqkv + (long)r * 3L * D + c, pack8(f));
+}
+
+template <int NKS, int KW>
+constexpr int bwd_smem() {
+  constexpr int NH = (NKS + 3) / 4, NO = (NKS + 1) / 2, KB = 32 * KW, TILES = 2 * NO;
+  constexpr int KSPLIT = KW >= TILES ? KW / TILES : 1;
+  constexpr int NTW = KSPLIT > 1 ? 1 : (TILES + KW - 1) / KW;
+  return 2 * NH * BQ * ROWB + 2 * NH * KB * ROWB + KB * ROWB + 2 * BQ * 4 + KW * BQ * 4 +
+         (KSPLIT > 1 ? (KSPLIT - 1) * TILES * 64 * 16 * 4 : 0) + (KSPLIT > 1 ? TILES : KW) * NTW * 16 * 64 * 4;
+}
+
+int nks_for(int hd);
+int nks_for_bwd(int hd) { return nks_for(hd); }
+
+int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
+int bwd_keys_per_block(int hd) { return nks_for_bwd(hd) > 4 ? 128 : 256; }
+
+// Persistent mode (one workgroup per (b, h), dQ summed in place) when B*H fills the chip's
+// workgroup slots in near-whole rounds (one 512-thread workgroup per CU); otherwise partial
+// mode: one workgroup per (key block, b, h), heaviest key blocks first, and a finalize pass.
+int g_bwd_mode = 0;  // 0 auto, 1 force persistent, 2 force partial (tests)
+
+bool bwd_persistent(int B, int T, int H) {
+  if (g_bwd_mode) return g_bwd_mode == 1;
+  const int cus = num_cus();
+  const int bh = B * H;
+  if ((T + 127) / 128 <= 1) return true;  // one key block: nothing to split
+  const int rounds = (bh + cus - 1) / cus;
+  return (double)bh / ((double)rounds * cus) >= 0.9;
+}
+
+template <int NKS, int KW>
+void launch_bwd(const AttnArgs& a, hipStream_t stream) {
+  constexpr int smem = bwd_smem<NKS, KW>();
+  static_assert(smem <= 160 * 1024, "attention backward LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)attn_bwd_kernel<NKS, KW>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  const int nkb = (a.T + 32 * KW - 1) / (32 * KW);
+  attn_bwd_kernel<NKS, KW><<<a.B * a.H * (a.dq_part ? nkb : 1), 64 * KW, smem, stream>>>(a);
+}
+
+int nks_for(int hd) {
+  const int k = (hd + 15) / 16;
+  return k <= 4 ? k : (k <= 6 ? 6 : 8);
+}
+
+}  // namespace
+
+namespace mg {
+
+size_t attention_dropout_mask_words(int B, int T, int H) {
+  return (size_t)B * H * T * 2 * ((T + 63) / 64);
+}
+
+int attention_dropout_threshold(float p) {
+  // 8-bit dropout threshold (as FlashAttention does): effective p = thr / 256
+  if (!(p > 0.f)) return 0;
+  int thr = (int)lrintf(p * 256.f);
+  return thr < 1 ? 1 : (thr > 255 ? 255 : thr);
+}
+
+void attention_dropout_mask(uint32_t* dmask, int B, int T, int H, float p, uint64_t seed,
+                            hipStream_t stream) {
+  const int thr = attention_dropout_threshold(p);
+  if (!thr) return;
+  const int ntw = 2 * ((T + 63) / 64);
+  attn_dropmask_kernel<<<dim3((unsigned)(B * H), (unsigned)cdiv(T, 256)), 256, 0, stream>>>(
+      dmask, B * H, T, ntw, seed, graph_seed_ofs(), (uint32_t)thr);
+}
+
+void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, uint32_t* dmask, int B, int T, int H,
+                   int hd, float p, uint64_t seed, hipStream_t stream) {
+  AttnArgs a{};
+  a.B = B; a.T = T; a.H = H; a.hd = hd; a.D = H * hd;
+  a.scale_log2 = 1.4426950408889634f / sqrtf((float)hd);
+  a.thr = dmask ? (uint32_t)attention_dropout_threshold(p) : 0u;
+  a.dscale = a.thr ? 256.f / (256.f - (float)a.thr) : 1.f;
+  a.qkv = qkv; a.out = out; a.lse = lse; a.dmask = dmask;
+  if (a.thr) attention_dropout_mask(dmask, B, T, H, p, seed, stream);
+  const int grid = cdiv(T, 128) * B * H;
+  switch (nks_for(hd)) {
+    case 1: attn_fwd_kernel<1><<<grid, 256, 0, stream>>>(a); break;
+    case 2: attn_fwd_kernel<2><<<grid, 256, 0, stream>>>(a); break;
+    case 3: attn_fwd_kernel<3><<<grid, 256, 0, stream>>>(a); break;
+    case 4: attn_fwd_kernel<4><<<grid, 256, 0, stream>>>(a); break;
+    case 6: attn_fwd_kernel<6><<<grid, 256, 0, stream>>>(a); break;
+    default: attn_fwd_kernel<8><<<grid, 256, 0, stream>>>(a); break;
+  }
+}
+
+void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse,
+                   const uint32_t* dmask, float* delta, float* dq, bf16_t* dqkv, int B, int T, int H,
+                   int hd, float p, uint64_t seed, hipStream_t stream) {
+  (void)seed;
+  AttnArgs a{};
+  a.B = B; a.T = T; a.H = H; a.hd = hd; a.D = H * hd;
+  a.scale_log2 = 1.4426950408889634f / sqrtf((float)hd);
+  a.thr = dmask ? (uint32_t)attention_dropout_threshold(p) : 0u;
+  a.dscale = a.thr ? 256.f / (256.f - (float)a.thr) : 1.f;
+  a.qkv = qkv; a.out = dqkv; a.lse = const_cast<float*>(lse); a.dout = dout; a.delta = delta;
+  a.dq = dq; a.dqkv = dqkv; a.dmask = dmask;
+  const bool persistent = bwd_persistent(B, T, H);
+  a.dq_part = persistent ? 0 : (long)B * T * H * hd;
+  int lg = 0;
+  while ((8 << lg) < hd) ++lg;
+  const long nthreads = (long)B * T * H << lg;
+  attn_bwd_pre_kernel<<<(unsigned)cdiv(nthreads, 256), 256, 0, stream>>>(dout, out, delta, B * T, T, H, hd, lg);
+  switch (nks_for(hd)) {
+    case 1: launch_bwd<1, 8>(a, stream); break;
+    case 2: launch_bwd<2, 8>(a, stream); break;
+    case 3: launch_bwd<3, 8>(a, stream); break;
+    case 4: launch_bwd<4, 8>(a, stream); break;
+    case 6: launch_bwd<6, 4>(a, stream); break;
+    default: launch_bwd<8, 4>(a, stream); break;
+  }
+  if (!persistent) {
+    const long n8 = (long)B * T * (H * hd / 8);
+    attn_dq_finalize_kernel<<<(unsigned)cdiv(n8, 256), 256, 0, stream>>>(
+        dq, dqkv, B * T, H * hd, T, bwd_keys_per_block(hd), a.dq_part, 0.6931471805599453f);
+  }
+}
+
+void attention_set_bwd_mode(int mode) { g_bwd_mode = mode; }
+
+size_t attention_bwd_workspace_floats(int B, int T, int H, int hd) {
+  const size_t one = (size_t)B * T * H * hd;
+  if (bwd_persistent(B, T, H)) return one;
+  const int kb = bwd_keys_per_block(hd);
+  return one * (size_t)((T + kb - 1) / kb);
+}
+
+}  // namespace mg

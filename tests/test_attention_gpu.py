@@ -9,12 +9,13 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.fixture(autouse=True, params=[0, 1], ids=["bwd256", "bwd128"])
-def bwd_variant(request):
-    """Run every test under both backward kernels (256-key and 128-key workgroups)."""
-    ext().attention_set_bwd_variant(request.param)
+@pytest.fixture(autouse=True, params=[1, 2], ids=["bwd_persistent", "bwd_partials"])
+def bwd_mode(request):
+    """Every test under both backward schedules: one workgroup per (b, h) summing dQ in place,
+    and one workgroup per (key block, b, h) with dQ partials + a finalize pass."""
+    ext().attention_set_bwd_mode(request.param)
     yield request.param
-    ext().attention_set_bwd_variant(0)
+    ext().attention_set_bwd_mode(0)
 
 
 def _split(qkv, B, T, H):
@@ -25,7 +26,9 @@ def _split(qkv, B, T, H):
 
 
 @pytest.mark.parametrize("B,T,H,hd", [(2, 128, 3, 64), (1, 200, 2, 64), (2, 1024, 2, 64), (2, 256, 4, 32),
-                                      (1, 96, 3, 16), (1, 64, 1, 64)])
+                                      (1, 96, 3, 16), (1, 64, 1, 64), (1, 300, 2, 128), (2, 200, 2, 96),
+                                      (1, 520, 2, 80), (1, 130, 2, 48), (1, 200, 3, 8), (1, 777, 1, 24),
+                                      (1, 256, 2, 112)])
 def test_attention_fwd_bwd(B, T, H, hd):
     C = ext()
     torch.manual_seed(0)
@@ -75,9 +78,8 @@ def test_attention_dropout_deterministic():
     dout = torch.randn_like(o1)
     d1 = C.attention_bwd(qkv, o1, dout, l1, m1, B, T, H, 0.1, 42)
     d2 = C.attention_bwd(qkv, o1, dout, l1, m2, B, T, H, 0.1, 42)
-    D = H * hd  # dK/dV are register-accumulated: bitwise reproducible; dQ uses fp32 atomics
-    assert torch.equal(d1[:, D:], d2[:, D:]) and torch.isfinite(d1.float()).all()
-    torch.testing.assert_close(d1[:, :D].float(), d2[:, :D].float(), atol=1e-2, rtol=1e-2)
+    # every gradient is register / workgroup-accumulated (no atomics): bitwise reproducible
+    assert torch.equal(d1, d2) and torch.isfinite(d1.float()).all()
 
 
 def test_attention_dropout_gradient_directional():
@@ -99,16 +101,38 @@ def test_attention_dropout_gradient_directional():
 
 
 def _dense_keep(mask, B, T, H):
-    """Dense [B, H, T, T] keep matrix from the forward's keep-bit words (layout: attention.hip)."""
-    ntiles = (T + 63) // 64
-    words = mask.view(B * H * T, ntiles * 2).to(torch.int64) & 0xFFFFFFFF
+    """Dense [B, H, T(query), T(key)] keep matrix from the keep-bit words (layout and bit order:
+    attention_train.hip attn_dropmask_kernel; words of tiles past the diagonal are unspecified)."""
+    ntw = 2 * ((T + 63) // 64)
+    words = mask.view(B * H, ntw, T).to(torch.int64) & 0xFFFFFFFF  # [bh, j, q]
     key = torch.arange(T, device=mask.device)
-    t, kk = key // 64, key % 64
-    col = t * 2 + ((kk >> 2) & 1)
-    el = ((kk & 32) >> 1) | (kk & 3) | (((kk >> 3) & 3) << 2)  # the lane's element index
-    bit = 8 * (el & 3) + (el >> 2)
-    w = words[:, col]  # [BHT, T]
-    return ((w >> bit) & 1).view(B, H, T, T).float()
+    kk = key % 64
+    j = (key // 64) * 2 + ((kk >> 2) & 1)
+    e = 16 * (kk >> 5) + 4 * ((kk >> 3) & 3) + (kk & 3)  # the forward lane's value index
+    bit = 8 * (e & 3) + (e >> 2)
+    w = words[:, j, :]  # [bh, key, q]
+    return ((w >> bit[None, :, None]) & 1).transpose(1, 2).reshape(B, H, T, T).float()
+
+
+@pytest.mark.parametrize("hd", [8, 16, 24, 32, 48, 64, 80, 96, 112, 128])
+def test_attention_fwd_head_dims(hd):
+    """Forward for every head dim the kernels take (multiples of 8 up to 128; hd > 64 uses two
+    64-column LDS halves), with and without dropout, vs the fp32 reference (exact keep mask)."""
+    C = ext()
+    B, T, H = 2, 200, 2
+    torch.manual_seed(hd)
+    D = H * hd
+    qkv = torch.randn(B * T, 3 * D, device=DEV).to(torch.bfloat16)
+    q, k, v = _split(qkv, B, T, H)
+    att = (q @ k.transpose(-1, -2)) / hd ** 0.5
+    att = att.masked_fill(~torch.ones(T, T, dtype=torch.bool, device=DEV).tril(), float("-inf"))
+    for p in (0.0, 0.1):
+        out, lse, mask = C.attention_fwd(qkv, B, T, H, p, 5)
+        keep = _dense_keep(mask, B, T, H) * (256.0 / (256 - round(p * 256))) if p > 0 else 1.0
+        ref = ((att.softmax(-1) * keep) @ v).transpose(1, 2).reshape(B * T, D)
+        torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=3e-2)
+        lse_ref = torch.logsumexp(att, -1) / torch.log(torch.tensor(2.0))
+        torch.testing.assert_close(lse.view(B, H, T), lse_ref, atol=2e-2, rtol=1e-3)
 
 
 @pytest.mark.parametrize("T", [128, 320])
