@@ -453,7 +453,8 @@ at::Tensor attention_decode(const at::Tensor& qkv_new, const at::Tensor& cache, 
   TORCH_CHECK(cache.dim() == 3, "cache must be [B, Tmax, 3D]");
   const int64_t B = cache.size(0), Tmax = cache.size(1), D3 = cache.size(2), D = D3 / 3;
   TORCH_CHECK(qkv_new.numel() == B * D3 && D % H == 0, "attention_decode: shape mismatch");
-  TORCH_CHECK(pos >= 0 && pos < Tmax && (D / H) % 8 == 0 && D / H <= 64, "attention_decode: pos / head dim");
+  TORCH_CHECK(pos >= 0 && pos < Tmax && (D / H) % 8 == 0 && D / H <= 128, "attention_decode: pos / head dim");
+  TORCH_CHECK(Tmax <= 4096, "attention_decode: KV cache longer than 4096 positions");
   DevGuard g(cache.device());
   auto out = at::empty({B, D}, cache.options());
   const int* pd = nullptr;

@@ -3,10 +3,17 @@
 Granularity is chosen for the MI355X, not for module boundaries: one Function per transformer
 block (LN1 -> QKV GEMM+bias -> flash attention -> proj GEMM with fused bias+dropout+residual ->
 LN2 -> FC GEMM with fused bias+GELU -> proj GEMM with fused bias+dropout+residual), one for the
-embedding and one for final-LN + LM head + cross-entropy.  Every GEMM, norm, attention, loss and
-elementwise op is a hand-written HIP kernel; weight gradients are accumulated in fp32 straight
-into ``param.main_grad`` (see ``grads.py``) so the data-parallel engine can all-reduce a bucket
-the moment its last gradient lands.
+embedding and one for final-LN + LM head + cross-entropy.  Every norm, attention, loss and
+elementwise op, every GEMM with a fused epilogue (bias+GELU, bias+dropout+residual, GELU', and all
+weight gradients with their fp32 accumulation) is a hand-written HIP kernel.  The GEMMs with
+nothing to fuse -- the qkv projection (bias only), the three plain data gradients of a block and
+the LM head's forward and data gradient -- run on the library GEMM (hipBLASLt through torch.mm)
+once they are large (``_big``), as the project brief allows for plain library GEMMs: at those
+shapes hipBLASLt's main loop was 5-25 % faster than the W4 kernel (PERF.md).  ``MINGPT_QKV_BLAS=0
+MINGPT_DGRAD_BLAS=0 MINGPT_LMHEAD_BLAS=0`` puts every GEMM on gemm.hip (the all-HIP path, also
+tested and benchmarked).  Weight gradients are accumulated in fp32 straight into
+``param.main_grad`` (see ``grads.py``) so the data-parallel engine can all-reduce a bucket the
+moment its last gradient lands.
 
 Reference anchors: block structure ``/root/reference/mingpt/model.py:171-189`` (with D4/D5/D6
 fixed), embedding ``model.py:193-231``, head + loss ``model.py:309-320``.

@@ -9,7 +9,9 @@ epilogue fused where the data is produced.
                    epilogue: ``none`` | ``gelu_bwd`` (multiply by aux = GELU'(z) from the forward)
 * ``gemm_tn_acc``  C[N,K] += A[M,N]^T @ B[M,K] (weight gradient, fp32 accumulate into main_grad)
 
-All three run on the hand-written MFMA kernel in ``csrc/kernels/gemm.hip`` (``_C.gemm``).
+All three run on the hand-written MFMA kernels in ``csrc/kernels/gemm.hip`` (``_C.gemm``).  The
+training step (``ops/fused.py``) routes the large epilogue-free GEMMs to hipBLASLt instead (see
+its module docstring; ``MINGPT_*_BLAS=0`` keeps them here).
 """
 from __future__ import annotations
 

@@ -177,3 +177,26 @@ def test_attention_dropout_keep_rate(p):
     _, _, mask2 = C.attention_fwd(qkv, B, T, H, p, 6)
     assert (keep != _dense_keep(mask2, B, T, H))[..., causal].float().mean().item() > 0.1  # seed matters
 
+
+
+@pytest.mark.parametrize("hd", [64, 128, 24])
+def test_attention_decode_split_keys(hd, bwd_mode):
+    """Split-key decode attention (workgroups over key ranges, last one combines) vs fp32
+    softmax(q K^T) V over keys 0..pos, with this step's K/V appended at row pos; repeated calls
+    (the per-(b, h) counters must come back to zero)."""
+    C = ext()
+    B, H, Tmax = 3, 2, 700
+    D = H * hd
+    torch.manual_seed(hd)
+    cache = torch.randn(B, Tmax, 3 * D, device=DEV).to(torch.bfloat16)
+    for pos in (0, 63, 64, 500, 699, 64):
+        qkv = torch.randn(B, 3 * D, device=DEV).to(torch.bfloat16)
+        c = cache.clone()
+        out = C.attention_decode(qkv, c, H, pos)
+        assert torch.equal(c[:, pos, D:], qkv[:, D:])  # K/V appended
+        q = qkv[:, :D].float().view(B, H, hd)
+        k = c[:, :pos + 1, D:2 * D].float().view(B, pos + 1, H, hd)
+        v = c[:, :pos + 1, 2 * D:].float().view(B, pos + 1, H, hd)
+        att = torch.einsum("bhd,bthd->bht", q, k) / hd ** 0.5
+        ref = torch.einsum("bht,bthd->bhd", att.softmax(-1), v).reshape(B, D)
+        torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)

@@ -157,3 +157,29 @@ def test_bpe_roundtrip_and_merges(tmp_path):
 def test_bpe_missing_files(tmp_path):
     with pytest.raises(FileNotFoundError):
         get_encoder(str(tmp_path / "nope"))
+
+
+def test_bucket_plan_tied_embedding_alone():
+    """FlatParamStore's bucket cut: a parameter at least a bucket large gets a bucket of its own
+    (GPT-2's tied wte, ready only after the embedding backward, does not hold back the smaller
+    gradients before it); buckets are contiguous, cover every parameter once, and a ZeRO-style
+    bucket_align pads each bucket to a multiple of it."""
+    from mingpt_distributed_amd.models import GPT, GPTConfig
+    from mingpt_distributed_amd.optim import FlatParamStore
+
+    m = GPT(GPTConfig(n_layer=2, n_head=2, n_embed=64, vocab_size=4096, block_size=64), verbose=False)
+    cap = 4096 * 64  # = numel(wte)
+    for align in (64, 4 * 64):
+        st = FlatParamStore(m, device="cpu", bucket_numel=cap, bucket_align=align)
+        seen = []
+        prev_end = 0
+        for s, e, ps in st.buckets:
+            assert s == prev_end and (e - s) % align == 0
+            prev_end = e
+            seen += ps
+            for i in ps:
+                assert s <= st.offsets[i] and st.offsets[i] + st.numels[i] <= e
+        assert sorted(seen) == list(range(len(st.params))) and prev_end == st.total
+        wte = st.by_name["transformer.wte.weight"]
+        (b,) = [ps for _, _, ps in st.buckets if wte in ps]
+        assert b == [wte]
