@@ -338,8 +338,10 @@ MG_DEVICE void bwd_softmax_grad(f32x16& s, f32x16& dp, const float (&dl)[16], co
       const bool kill = (mykey > q) | (q >= T);  // bitwise: no short-circuit branches
       p = kill ? 0.f : p;
     }
-    // no dropout: every keep word is all ones (set when staged), dscale = 1
-    const int keep = __builtin_amdgcn_sbfe((int)mwr[r], mw_bit, 1);  // 0 or -1
+    // no dropout: every keep word is all ones (set when staged), dscale = 1.  One v_bfe_i32 (the
+    // builtin became and + compare + select)
+    int keep;
+    asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(keep) : "v"(mwr[r]), "v"(mw_bit));
     s[r] = __int_as_float(__float_as_int(p) & keep);
     const float dpv = __int_as_float(__float_as_int(dp[r]) & keep);
     dp[r] = p * __builtin_fmaf(dpv, dscale, -dl[r]);
@@ -372,8 +374,9 @@ struct Stager {
 };
 
 // Key-block-parallel backward, one workgroup per (b, h) sweeping its key blocks in order.
-//  * KW waves = KB = 32 KW keys per block (K pre-scaled by log2(e)/sqrt(hd), and V, in LDS);
-//    each wave keeps dK^T / dV^T accumulators (keys on the lane) across the block's query sweep.
+//  * KW waves = KB = 32 KW keys per block (K pre-scaled by log2(e)/sqrt(hd) in LDS); each wave
+//    keeps its 32 keys' V rows (the dP~ B operand) and dK^T / dV^T accumulators (keys on the lane)
+//    in registers across the block's query sweep.
 //  * per 64-query tile (Q, dO, lse, delta, keep-words staged in LDS, the next tile prefetched in
 //    VGPRs): S and dP with the key on the lane, P and dS in registers feed dV^T += dO^T P and
 //    dK^T += Q^T dS directly (transposed reads of Q / dO); dS^T goes through LDS once for
@@ -385,7 +388,7 @@ struct Stager {
 //    the last block that reaches the tile: no per-key-block partial buffers, no finalize pass.
 //  * attention dropout: the forward's keep bits (attn_dropmask_kernel), one word per query and
 //    32-key half tile, staged 64 queries x KW words per tile.
-template <int NKS, int KW>
+template <int NKS, int KW, bool PERSIST>
 __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) {
   constexpr int NH = (NKS + 3) / 4, NO = (NKS + 1) / 2;
   constexpr int NT = 64 * KW, KB = 32 * KW;
@@ -393,7 +396,7 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
   constexpr int TILES = 2 * NO;                  // 32x32 dQ tiles of a 64-query tile
   constexpr int KSPLIT = KW >= TILES ? KW / TILES : 1;
   constexpr int OFF_Q = 0, OFF_DO = OFF_Q + NH * HQ, OFF_K = OFF_DO + NH * HQ;
-  constexpr int OFF_V = OFF_K + NH * HK, OFF_DS = OFF_V + NH * HK, OFF_L = OFF_DS + KB * ROWB;
+  constexpr int OFF_DS = OFF_K + NH * HK, OFF_L = OFF_DS + KB * ROWB;
   constexpr int OFF_MW = OFF_L + 2 * BQ * 4, OFF_P = OFF_MW + KW * BQ * 4;
   constexpr int OFF_PV = OFF_P + (KSPLIT > 1 ? (KSPLIT - 1) * TILES * 64 * 16 * 4 : 0);
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -409,7 +412,6 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
   const float* lseg = a.lse + (long)bh * a.T;
   const float* dlg = a.delta + (long)bh * a.T;
   char* sK = smem + OFF_K;
-  char* sV = smem + OFF_V;
   char* sdS = smem + OFF_DS;
   const float* sL = reinterpret_cast<const float*>(smem + OFF_L);
   const uint32_t* sMW = reinterpret_cast<const uint32_t*>(smem + OFF_MW);
@@ -430,11 +432,12 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
 
   // persistent mode (dq_part == 0): this workgroup sweeps every key block of its (b, h); partial
   // mode: workgroup = one key block (heaviest first), its dQ contribution stored as partial kb
-  const bool part = a.dq_part != 0;
+  constexpr bool part = !PERSIST;
   const int kb_lo = part ? blockIdx.x / BH : 0, kb_hi = part ? kb_lo + 1 : nkb;
   for (int kb = kb_lo; kb < kb_hi; ++kb) {
     const int kb0 = kb * KB;
     int mykey, wave_kmin;
+    bf16x8 vf[NKS];  // this wave's 32 keys' V rows: the B operand of dP~ = dO V^T
     {
       const int lane = threadIdx.x & 63, h32 = lane >> 5, l32 = lane & 31;
       mykey = kb0 + 32 * w + l32;
@@ -449,12 +452,14 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
         for (int j = 0; j < 8; ++j) f[j] *= a.scale_log2;
         rk[i] = pack8(f);
       }
-      uint4 rv[stk::N];
-      stk::load(rv, Vg, ld, kb0, a.T, a.hd);
-      __syncthreads();  // the previous block's readers of sK / sV are done
+      __syncthreads();  // the previous block's readers of sK are done
       stk::store(sK, rk);
-      stk::store(sV, rv);
-      (void)h32; (void)l32;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const int d = ks * 16 + 8 * h32;
+        const bool ok = mykey < a.T && d < a.hd;
+        vf[ks] = __builtin_bit_cast(bf16x8, ok ? ld16(Vg + (long)mykey * ld + d) : make_uint4(0, 0, 0, 0));
+      }
     }
     // this lane's dropout bit inside the keep words (attn_dropmask_kernel layout)
     const int mw_col = (w >> 1) * 2 + ((mykey >> 2) & 1);
@@ -512,7 +517,7 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
       // previous key blocks' dQ sums of this wave's tiles: LDS-DMA'd now (no registers held),
       // added after the dQ MFMAs (a load in the store loop exposed a memory latency per tile)
       float* pvs = reinterpret_cast<float*>(smem + OFF_PV) + (my_split == 0 ? w : 0) * NTW * 16 * 64;
-      if (!first && my_split == 0) {
+      if (PERSIST && !first && my_split == 0) {
 #pragma unroll
         for (int i = 0; i < NTW; ++i) {
           const int tt = tt0 + i * TSTEP;
@@ -568,8 +573,8 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
         for (int ks = 0; ks < NKS; ++ks) {  // S' = Q (cK)^T - lse ; dP~ = dO V^T
           sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_at(sQ + qs * 32 * ROWB, ro[ks]),
                                                          lds_row_at(sK, rk_[ks]), sacc, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_at(sdO + qs * 32 * ROWB, ro[ks]),
-                                                       lds_row_at(sV, rk_[ks]), dp, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_at(sdO + qs * 32 * ROWB, ro[ks]), vf[ks], dp,
+                                                       0, 0, 0);
         }
         // wave-uniform: only diagonal / past-T tiles pay for the causal mask
         if (wave_kmin + 31 > qsub0 || qsub0 + 31 >= a.T)
@@ -642,7 +647,7 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
         }
         const int d = n * 32 + l32;
         if (my_split == 0 && d < a.hd && qbase + qs * 32 + 31 >= kb0) {
-          if (!first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
+          if (PERSIST && !first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
           // row q0 + (r & 3) + 8 (r >> 2): one 64-bit base per lane, then uniform row strides
           const int q0 = qbase + qs * 32 + 4 * h32;
           const long roff = ((long)b * a.T + q0) * a.D + hh * a.hd + d;
@@ -652,7 +657,7 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
           for (int r = 0; r < 16; ++r) {
             const int dr = (r & 3) + 8 * (r >> 2);
             if (q0 + dr < a.T) {
-              const float v = first ? dq[r] : dq[r] + pvs[(i * 16 + r) * 64 + lane];
+              const float v = (!PERSIST || first) ? dq[r] : dq[r] + pvs[(i * 16 + r) * 64 + lane];
               if (last)
                 outq[(long)dr * ld] = f2bf(v * dq_scale);
               else
@@ -715,7 +720,7 @@ constexpr int bwd_smem() {
   constexpr int NH = (NKS + 3) / 4, NO = (NKS + 1) / 2, KB = 32 * KW, TILES = 2 * NO;
   constexpr int KSPLIT = KW >= TILES ? KW / TILES : 1;
   constexpr int NTW = KSPLIT > 1 ? 1 : (TILES + KW - 1) / KW;
-  return 2 * NH * BQ * ROWB + 2 * NH * KB * ROWB + KB * ROWB + 2 * BQ * 4 + KW * BQ * 4 +
+  return 2 * NH * BQ * ROWB + NH * KB * ROWB + KB * ROWB + 2 * BQ * 4 + KW * BQ * 4 +
          (KSPLIT > 1 ? (KSPLIT - 1) * TILES * 64 * 16 * 4 : 0) + (KSPLIT > 1 ? TILES : KW) * NTW * 16 * 64 * 4;
 }
 
@@ -738,9 +743,13 @@ int bwd_keys_per_block(int hd) { return nks_for_bwd(hd) > 4 ? 128 : 256; }
 // Persistent mode (one workgroup per (b, h), dQ summed in place) when B*H fills the chip's
 // workgroup slots in near-whole rounds (one 512-thread workgroup per CU); otherwise partial
 // mode: one workgroup per (key block, b, h), heaviest key blocks first, and a finalize pass.
-int g_bwd_mode = 0;  // 0 auto, 1 force persistent, 2 force partial (tests)
+int g_bwd_mode = -1;  // 0 auto, 1 force persistent, 2 force partial (tests, MINGPT_ATTN_BWD_MODE)
 
 bool bwd_persistent(int B, int T, int H) {
+  if (g_bwd_mode < 0) {
+    const char* e = getenv("MINGPT_ATTN_BWD_MODE");
+    g_bwd_mode = e ? atoi(e) : 0;
+  }
   if (g_bwd_mode) return g_bwd_mode == 1;
   const int cus = num_cus();
   const int bh = B * H;
@@ -755,11 +764,15 @@ void launch_bwd(const AttnArgs& a, hipStream_t stream) {
   static_assert(smem <= 160 * 1024, "attention backward LDS budget");
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)attn_bwd_kernel<NKS, KW>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    hipFuncSetAttribute((const void*)attn_bwd_kernel<NKS, KW, true>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    hipFuncSetAttribute((const void*)attn_bwd_kernel<NKS, KW, false>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
   const int nkb = (a.T + 32 * KW - 1) / (32 * KW);
-  attn_bwd_kernel<NKS, KW><<<a.B * a.H * (a.dq_part ? nkb : 1), 64 * KW, smem, stream>>>(a);
+  if (a.dq_part)
+    attn_bwd_kernel<NKS, KW, false><<<a.B * a.H * nkb, 64 * KW, smem, stream>>>(a);
+  else
+    attn_bwd_kernel<NKS, KW, true><<<a.B * a.H, 64 * KW, smem, stream>>>(a);
 }
 
 int nks_for(int hd) {
