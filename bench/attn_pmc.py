@@ -14,7 +14,8 @@ p = float(os.environ.get("ATTN_P", "0.1"))
 iters = int(os.environ.get("ATTN_ITERS", "2"))
 D = H * hd
 C = ext()
-C.attention_set_bwd_mode(int(os.environ.get("ATTN_BWD_MODE", "0")))
+if hasattr(C, "attention_set_bwd_mode"):  # older builds (A/B) have one schedule
+    C.attention_set_bwd_mode(int(os.environ.get("ATTN_BWD_MODE", "0")))
 qkv = torch.randn(B * T, 3 * D, device="cuda").to(torch.bfloat16)
 dout = torch.randn(B * T, D, device="cuda").to(torch.bfloat16)
 for _ in range(iters):

@@ -627,19 +627,20 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
         if constexpr (KSPLIT > 1) {  // key splits 1.. hand their partial tile to split 0 via LDS
           float* part = reinterpret_cast<float*>(smem + OFF_P);
           if (my_split > 0) {
-            float* pp = part + (((my_split - 1) * TILES + tt) * 64 + lane) * 16;
+            // [split][tile][g][lane] f32x4: consecutive lanes 16 B apart (conflict-free b128)
+            float* pp = part + ((my_split - 1) * TILES + tt) * 4 * 64 * 4 + lane * 4;
 #pragma unroll
             for (int g = 0; g < 4; ++g)
-              *reinterpret_cast<f32x4*>(pp + 4 * g) = f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
+              *reinterpret_cast<f32x4*>(pp + g * 64 * 4) = f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
           }
           __syncthreads();
           if (my_split == 0) {
 #pragma unroll
             for (int sp = 1; sp < KSPLIT; ++sp) {
-              const float* pp = part + (((sp - 1) * TILES + tt) * 64 + lane) * 16;
+              const float* pp = part + ((sp - 1) * TILES + tt) * 4 * 64 * 4 + lane * 4;
 #pragma unroll
               for (int g = 0; g < 4; ++g) {
-                const f32x4 x = *reinterpret_cast<const f32x4*>(pp + 4 * g);
+                const f32x4 x = *reinterpret_cast<const f32x4*>(pp + g * 64 * 4);
                 dq[4 * g] += x[0]; dq[4 * g + 1] += x[1]; dq[4 * g + 2] += x[2]; dq[4 * g + 3] += x[3];
               }
             }
@@ -653,16 +654,21 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
           const long roff = ((long)b * a.T + q0) * a.D + hh * a.hd + d;
           float* dqb = a.dq + (part ? kb * a.dq_part : 0) + roff;
           bf16_t* outq = a.dqkv + ((long)b * a.T + q0) * ld + hh * a.hd + d;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
+          auto put = [&](int r) {
             const int dr = (r & 3) + 8 * (r >> 2);
-            if (q0 + dr < a.T) {
-              const float v = (!PERSIST || first) ? dq[r] : dq[r] + pvs[(i * 16 + r) * 64 + lane];
-              if (last)
-                outq[(long)dr * ld] = f2bf(v * dq_scale);
-              else
-                dqb[(long)dr * a.D] = v;
-            }
+            const float v = (!PERSIST || first) ? dq[r] : dq[r] + pvs[(i * 16 + r) * 64 + lane];
+            if (last)
+              outq[(long)dr * ld] = f2bf(v * dq_scale);
+            else
+              dqb[(long)dr * a.D] = v;
+          };
+          if (qbase + BQ <= a.T) {  // whole tile inside the sequence: no per-row checks
+#pragma unroll
+            for (int r = 0; r < 16; ++r) put(r);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              if (q0 + (r & 3) + 8 * (r >> 2) < a.T) put(r);
           }
         }
       }
@@ -704,12 +710,22 @@ __global__ __launch_bounds__(256) void attn_dq_finalize_kernel(const float* __re
   const int r = (int)(i / d8);  // 32-bit operands: a cheap division
   const int c = (int)(i - (long)r * d8) * 8;
   const int np = (r % T) / KB + 1;
+  const float* src = dq + (long)r * D + c;
   float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
-  for (int k = 0; k < np; ++k) {
-    const float* src = dq + k * part + (long)r * D + c;
-    const float4 y0 = *reinterpret_cast<const float4*>(src), y1 = *reinterpret_cast<const float4*>(src + 4);
-    x0.x += y0.x; x0.y += y0.y; x0.z += y0.z; x0.w += y0.w;
-    x1.x += y1.x; x1.y += y1.y; x1.z += y1.z; x1.w += y1.w;
+  for (int k = 0; k < np; k += 4) {  // four partials' loads in flight before the adds
+    float4 y[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = k + u < np;
+      const float* s = src + (long)(ok ? k + u : k) * part;
+      y[u][0] = ok ? *reinterpret_cast<const float4*>(s) : make_float4(0.f, 0.f, 0.f, 0.f);
+      y[u][1] = ok ? *reinterpret_cast<const float4*>(s + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      x0.x += y[u][0].x; x0.y += y[u][0].y; x0.z += y[u][0].z; x0.w += y[u][0].w;
+      x1.x += y[u][1].x; x1.y += y[u][1].y; x1.z += y[u][1].z; x1.w += y[u][1].w;
+    }
   }
   const float f[8] = {x0.x * sc, x0.y * sc, x0.z * sc, x0.w * sc, x1.x * sc, x1.y * sc, x1.z * sc, x1.w * sc};
   st16(dqkv + (long)r * 3L * D + c, pack8(f));
@@ -740,22 +756,21 @@ int num_cus() {
 
 int bwd_keys_per_block(int hd) { return nks_for_bwd(hd) > 4 ? 128 : 256; }
 
-// Persistent mode (one workgroup per (b, h), dQ summed in place) when B*H fills the chip's
-// workgroup slots in near-whole rounds (one 512-thread workgroup per CU); otherwise partial
-// mode: one workgroup per (key block, b, h), heaviest key blocks first, and a finalize pass.
-int g_bwd_mode = -1;  // 0 auto, 1 force persistent, 2 force partial (tests, MINGPT_ATTN_BWD_MODE)
+// Key-block mode (one workgroup per (key block, b, h), heaviest key blocks first, then a finalize
+// pass over the fp32 dQ partials) by default: measured in the GPT-2 step (B=64, T=1024, hd=64;
+// profiles/round2_attn_bwd_modes.txt) it beats the persistent schedule (one workgroup per (b, h)
+// sweeping its key blocks, dQ summed in place) even where B*H fills the chip in whole rounds --
+// the in-place read-add-store of dQ costs the persistent kernel more than the finalize pass.
+// Persistent mode is used when there is a single key block (no partial sum to form).
+int g_bwd_mode = -1;  // 0 auto, 1 force persistent, 2 force key-block (tests, MINGPT_ATTN_BWD_MODE)
 
-bool bwd_persistent(int B, int T, int H) {
+bool bwd_persistent(int T, int hd) {
   if (g_bwd_mode < 0) {
     const char* e = getenv("MINGPT_ATTN_BWD_MODE");
     g_bwd_mode = e ? atoi(e) : 0;
   }
   if (g_bwd_mode) return g_bwd_mode == 1;
-  const int cus = num_cus();
-  const int bh = B * H;
-  if ((T + 127) / 128 <= 1) return true;  // one key block: nothing to split
-  const int rounds = (bh + cus - 1) / cus;
-  return (double)bh / ((double)rounds * cus) >= 0.9;
+  return T <= bwd_keys_per_block(hd);
 }
 
 template <int NKS, int KW>
@@ -835,7 +850,7 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
   a.dscale = a.thr ? 256.f / (256.f - (float)a.thr) : 1.f;
   a.qkv = qkv; a.out = dqkv; a.lse = const_cast<float*>(lse); a.dout = dout; a.delta = delta;
   a.dq = dq; a.dqkv = dqkv; a.dmask = dmask;
-  const bool persistent = bwd_persistent(B, T, H);
+  const bool persistent = bwd_persistent(T, hd);
   a.dq_part = persistent ? 0 : (long)B * T * H * hd;
   int lg = 0;
   while ((8 << lg) < hd) ++lg;
@@ -860,7 +875,7 @@ void attention_set_bwd_mode(int mode) { g_bwd_mode = mode; }
 
 size_t attention_bwd_workspace_floats(int B, int T, int H, int hd) {
   const size_t one = (size_t)B * T * H * hd;
-  if (bwd_persistent(B, T, H)) return one;
+  if (bwd_persistent(T, hd)) return one;
   const int kb = bwd_keys_per_block(hd);
   return one * (size_t)((T + kb - 1) / kb);
 }

@@ -105,18 +105,19 @@ class GPTConfig:
         return self.n_embed // self.n_head
 
     # shapes the gfx950 kernels take (checked on the host before the first GPU launch)
-    GPU_MAX_HEAD_DIM = 64
+    GPU_MAX_HEAD_DIM = 128
 
     def gpu_unsupported(self) -> Optional[str]:
         """Why the GPU kernels cannot run this config, or None.  Every kernel reads rows in
-        16-byte (8 x bf16) vectors and the attention kernels are instantiated per head dim."""
+        16-byte (8 x bf16) vectors; the attention kernels take any head dim that is a multiple of 8
+        up to 128 (csrc/kernels/attention_train.hip ``nks_for``; decode: attention.hip)."""
         if self.n_embed is None or self.n_head is None:
             return "config not resolved"
         hd = self.n_embed // self.n_head
         if self.n_embed % 8:
             return f"n_embed={self.n_embed} must be a multiple of 8 on the GPU"
-        if hd % 8 or hd > self.GPU_MAX_HEAD_DIM or hd & (hd - 1):
-            return (f"head dim {hd} (n_embed/n_head) must be a power of two in [8, "
+        if hd % 8 or hd > self.GPU_MAX_HEAD_DIM:
+            return (f"head dim {hd} (n_embed/n_head) must be a multiple of 8 in [8, "
                     f"{self.GPU_MAX_HEAD_DIM}] on the GPU")
         return None
 

@@ -146,3 +146,14 @@ def test_gpu_shape_validation_is_early():
     assert "multiple of 8" in bad.gpu_unsupported()
     with pytest.raises(ValueError, match="not supported by the GPU kernels"):
         bad.check_gpu_support()
+
+
+def test_gpu_head_dims_accepted():
+    """Head dims the kernels take (multiples of 8 up to 128, power of two or not) pass the host
+    check; 136 (> 128) and 20 (not a multiple of 8) do not."""
+    from mingpt_distributed_amd.models import GPTConfig
+
+    for hd in (8, 48, 64, 80, 96, 128):
+        assert GPTConfig(n_layer=1, n_head=2, n_embed=2 * hd).resolve().gpu_unsupported() is None, hd
+    assert "multiple of 8" in GPTConfig(n_layer=1, n_head=2, n_embed=272).resolve().gpu_unsupported()
+    assert "multiple of 8" in GPTConfig(n_layer=1, n_head=2, n_embed=40).resolve().gpu_unsupported()

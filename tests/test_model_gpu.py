@@ -17,10 +17,12 @@ def _cfg(**kw):
     return GPTConfig(**base)
 
 
-@pytest.mark.parametrize("hd,gs", [(64, 1.0), (32, 1.0), (64, 0.25)])
-def test_forward_backward_matches_reference(hd, gs):
+@pytest.mark.parametrize("hd,nh,gs", [(64, 2, 1.0), (32, 4, 1.0), (64, 2, 0.25), (48, 3, 1.0),
+                                      (96, 2, 1.0), (128, 2, 1.0)])
+def test_forward_backward_matches_reference(hd, nh, gs):
+    """Whole model (non-power-of-two and > 64 head dims included) vs the fp32 reference."""
     torch.manual_seed(0)
-    cpu = GPT(_cfg(n_head=128 // hd), verbose=False)
+    cpu = GPT(_cfg(n_head=nh, n_embed=nh * hd), verbose=False)
     gpu = copy.deepcopy(cpu).cuda().to(torch.bfloat16)
     # reference uses the bf16-rounded weights in fp32
     with torch.no_grad():
