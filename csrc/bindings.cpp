@@ -72,17 +72,24 @@ at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Te
 }
 
 // ------------------------------------------------------------------------------- embedding
+// pos_dev (int32 [1], optional; decode with T == 1): the position row of wpe is read on the device
 at::Tensor embedding_fwd(const at::Tensor& idx, const at::Tensor& wte, const at::Tensor& wpe,
-                         double p, int64_t seed) {
+                         double p, int64_t seed, const c10::optional<at::Tensor>& pos_dev) {
   CHECK_I64(idx); CHECK_BF16(wte); CHECK_BF16(wpe); CHECK_CONTIG(idx);
   CHECK_CONTIG(wte); CHECK_CONTIG(wpe);
   TORCH_CHECK(idx.dim() == 2, "idx must be [B, T]");
   const int64_t B = idx.size(0), T = idx.size(1), D = wte.size(1);
   TORCH_CHECK(D % 8 == 0 && wpe.size(1) == D && T <= wpe.size(0), "embedding: shape mismatch");
+  const int* pd = nullptr;
+  if (pos_dev.has_value()) {
+    TORCH_CHECK(T == 1 && pos_dev->scalar_type() == at::kInt && pos_dev->is_cuda(),
+                "embedding_fwd: pos_dev (int32 cuda) is for one-token decode steps");
+    pd = pos_dev->data_ptr<int>();
+  }
   DevGuard g(idx.device());
   auto out = at::empty({B, T, D}, wte.options());
   mg::embedding_fwd(idx.data_ptr<int64_t>(), bp(wte), bp(wpe), bp(out), (int)(B * T), (int)T,
-                    (int)D, (int)wte.size(0), (float)p, (uint64_t)seed, cur_stream());
+                    (int)D, (int)wte.size(0), (float)p, (uint64_t)seed, cur_stream(), pd);
   return out;
 }
 
@@ -422,7 +429,8 @@ at::Tensor attention_bwd(const at::Tensor& qkv, const at::Tensor& out, const at:
 // y[B, ldy] (ldy >= N) = epi(x[B, K] @ W[N, K]^T): the decode-time projection (gemv.hip)
 at::Tensor gemv(const at::Tensor& x, const at::Tensor& W, int64_t epi, const c10::optional<at::Tensor>& bias,
                 const c10::optional<at::Tensor>& resid, int64_t ldy, const c10::optional<at::Tensor>& lnw,
-                const c10::optional<at::Tensor>& lnb, double eps) {
+                const c10::optional<at::Tensor>& lnb, double eps, const c10::optional<at::Tensor>& am_tok,
+                const c10::optional<at::Tensor>& am_pos, const c10::optional<at::Tensor>& am_seq) {
   CHECK_BF16(x); CHECK_BF16(W); CHECK_CONTIG(x); CHECK_CONTIG(W);
   const int64_t K = W.size(1), N = W.size(0), B = x.numel() / K;
   TORCH_CHECK(x.size(-1) == K && mg::gemv_supported((int)B, (int)K), "gemv: B <= 8, K % 8 == 0, K <= 4096");
@@ -440,9 +448,50 @@ at::Tensor gemv(const at::Tensor& x, const at::Tensor& W, int64_t epi, const c10
     TORCH_CHECK(lnw->numel() == K && lnb->numel() == K, "gemv: LayerNorm size");
   }
   DevGuard g(x.device());
+  mg::GemvArgmax am{};
+  if (am_tok.has_value()) {
+    // greedy decode: fused argmax (the LM head, N > 8192 rows) -> am_tok [B] int64, am_seq[b, pos+1],
+    // *am_pos += 1.  Workspace: one 8-byte partial per (row, workgroup) and an arrival counter,
+    // allocated outside graph capture (the first, eager call) and left zeroed by the kernel.
+    TORCH_CHECK(N > 8192 && epi == 0, "gemv argmax: LM-head shape (N > 8192, no epilogue)");
+    TORCH_CHECK(am_tok->scalar_type() == at::kLong && am_tok->numel() == B && am_tok->is_cuda() &&
+                am_pos.has_value() && am_pos->scalar_type() == at::kInt && am_pos->is_cuda(),
+                "gemv argmax: am_tok int64 [B], am_pos int32 [1]");
+    static unsigned long long* part = nullptr;
+    static unsigned* cnt = nullptr;
+    static size_t part_n = 0, cnt_n = 0;
+    const size_t need = mg::gemv_argmax_part_words((int)B, (int)N), needc = mg::gemv_argmax_counters((int)N);
+    if (need > part_n || needc > cnt_n) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      hipStreamIsCapturing(cur_stream(), &cs);
+      TORCH_CHECK(cs == hipStreamCaptureStatusNone, "gemv argmax: first call must not be inside a graph capture");
+      if (need > part_n) {
+        if (part) hipFree(part);
+        hipMalloc(&part, need * sizeof(unsigned long long));
+        part_n = need;
+      }
+      if (needc > cnt_n) {
+        if (cnt) hipFree(cnt);
+        hipMalloc(&cnt, needc * sizeof(unsigned));
+        hipMemset(cnt, 0, needc * sizeof(unsigned));
+        cnt_n = needc;
+      }
+      hipDeviceSynchronize();
+    }
+    am.part = part; am.cnt = cnt;
+    am.tok = am_tok->data_ptr<int64_t>();
+    am.pos = am_pos->data_ptr<int>();
+    if (am_seq.has_value()) {
+      TORCH_CHECK(am_seq->scalar_type() == at::kLong && am_seq->dim() == 2 && am_seq->size(0) == B &&
+                  am_seq->is_contiguous(), "gemv argmax: am_seq int64 [B, L]");
+      am.seq = am_seq->data_ptr<int64_t>();
+      am.seq_ld = am_seq->size(1);
+    }
+  }
   auto y = at::empty({B, ldy}, x.options());
   mg::gemv(bp(x), bp(W), bp(y), (int)B, (int)N, (int)K, ldy, bias.has_value() ? bp(*bias) : nullptr,
-           epi == 3 ? bp(*resid) : nullptr, (int)epi, cur_stream(), bp_opt(lnw), bp_opt(lnb), (float)eps);
+           epi == 3 ? bp(*resid) : nullptr, (int)epi, cur_stream(), bp_opt(lnw), bp_opt(lnb), (float)eps,
+           am_tok.has_value() ? &am : nullptr);
   return y;
 }
 
@@ -473,7 +522,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mingpt_distributed_amd gfx950 kernels";
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
-  m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_fwd", &embedding_fwd, py::arg("idx"), py::arg("wte"), py::arg("wpe"), py::arg("p"),
+        py::arg("seed"), py::arg("pos_dev") = py::none());
   // debug builds: OR of the device error words (1/2 = token id out of range in embedding fwd/bwd,
   // 4 = cross-entropy target >= V), cleared on read; always 0 in release builds
   m.def("debug_error_bits", []() -> int64_t { return (int64_t)mg::debug_error_bits(); });
@@ -511,7 +561,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attention_bwd", &attention_bwd);
   m.def("gemv", &gemv, py::arg("x"), py::arg("W"), py::arg("epi"), py::arg("bias") = py::none(),
         py::arg("resid") = py::none(), py::arg("ldy") = 0, py::arg("lnw") = py::none(),
-        py::arg("lnb") = py::none(), py::arg("eps") = 1e-5);
+        py::arg("lnb") = py::none(), py::arg("eps") = 1e-5, py::arg("am_tok") = py::none(),
+        py::arg("am_pos") = py::none(), py::arg("am_seq") = py::none());
   m.def("gemv_supported", &mg::gemv_supported);
   m.def("attention_decode", &attention_decode, py::arg("qkv_new"), py::arg("cache"), py::arg("H"),
         py::arg("pos"), py::arg("pos_dev") = py::none());

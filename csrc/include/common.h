@@ -50,6 +50,12 @@ MG_DEVICE uint4 pack8(const float (&f)[8]) {
 }
 
 MG_DEVICE uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
+// non-temporal 16-byte load (streamed-once weights: decode GEMV)
+MG_DEVICE uint4 ld16_nt(const void* p) {
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
 
 // hipGraph mode: a captured kernel's seed argument is an offset into a per-replay stream whose
 // counter lives in device memory (incremented inside the graph), so every replay draws new

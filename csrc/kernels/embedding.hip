@@ -21,14 +21,15 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict_
                                                       bf16_t* __restrict__ out, int M, int T, int D, int V,
                                                       unsigned int* __restrict__ err,
                                                       uint64_t seed, uint32_t thr, float scale,
-                                                      int use_dropout, const uint64_t* sofs) {
+                                                      int use_dropout, const uint64_t* sofs,
+                                                      const int* __restrict__ pos_dev) {
   const int lane = threadIdx.x & 63;
   const long m = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= M) return;
   seed = eff_seed(seed, sofs);
   long tok = idx[m];
   MG_CHECK_INDEX(tok, tok >= 0 && tok < V, 0, err, 1u)
-  const int t = (int)(m % T);
+  const int t = pos_dev ? *pos_dev : (int)(m % T);  // decode step: one token at a device position
   for (int c = lane * 8; c < D; c += 512) {
     float a[8], p[8];
     unpack8(ld16(wte + tok * D + c), a);
@@ -106,11 +107,11 @@ __global__ __launch_bounds__(64) void emb_bwd_wpe_kernel(const bf16_t* __restric
 namespace mg {
 
 void embedding_fwd(const int64_t* idx, const bf16_t* wte, const bf16_t* wpe, bf16_t* out, int M,
-                   int T, int D, int V, float p, uint64_t seed, hipStream_t stream) {
+                   int T, int D, int V, float p, uint64_t seed, hipStream_t stream, const int* pos_dev) {
   const uint32_t thr = dropout_threshold8(p);  // the 8-bit residual-stream mask (common.h)
   emb_fwd_kernel<<<cdiv(M, 4), 256, 0, stream>>>(idx, wte, wpe, out, M, T, D, V, debug_err_word(), seed, thr,
                                                  dropout_scale8(thr), p > 0.f,
-                                                 graph_seed_ofs());
+                                                 graph_seed_ofs(), pos_dev);
 }
 
 void embedding_bwd(const int64_t* idx, const bf16_t* dout, float* dwte, float* dwpe, int M, int T,

@@ -13,7 +13,13 @@
 //     FMA against the B vectors from LDS;
 //   * the lanes of a row fold with xor-shuffles; the row's first lane writes y[b, n] with the same
 //     fused epilogues as gemm.hip's forward (bias | bias + GELU | residual + bias), no dropout
-//     (inference).
+//     (inference);
+//   * weights are read non-temporally (streamed once per token; MI355X_MICROARCH launches-baseline:
+//     nt weight loads ~11 % faster per decode layer);
+//   * greedy decode (LM head): the argmax of the logits is fused -- each workgroup publishes its
+//     best (value, index) key with agent-scope stores, the last one to arrive reduces them and
+//     writes the next token and position on the device, so a captured decode step can be replayed
+//     back to back with no host round trip per token.
 #include "common.h"
 #include "kernels.h"
 
@@ -24,6 +30,101 @@ namespace {
 constexpr int kGemvMaxB = 8;
 constexpr int kGemvMaxK = 4096;  // B x K bf16 of x must fit the LDS staging buffer
 
+// order-preserving key of a float (larger float -> larger key), index in the low half inverted
+// so that the max key is the FIRST index among equal values (torch.argmax)
+MG_DEVICE unsigned long long amax_key(float v, int n) {
+  const uint32_t u = __float_as_uint(v);
+  const uint32_t k = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((unsigned long long)k << 32) | (uint32_t)(0xffffffffu - (uint32_t)n);
+}
+MG_DEVICE unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
+MG_DEVICE unsigned long long wave_umax64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned lo = __shfl_xor((unsigned)v, o, 64), hi = __shfl_xor((unsigned)(v >> 32), o, 64);
+    v = umax64(v, ((unsigned long long)hi << 32) | lo);
+  }
+  return v;
+}
+
+// Fused greedy argmax over the 16 rows of this workgroup, then across workgroups in two levels
+// (groups of 64 workgroups, then the groups): thousands of arrivals on ONE counter serialise at
+// ~88 per us (MI355X_MICROARCH 'dequeue'), one counter per group keeps each word at <= 64.
+// Hand-off as in attn_decode_kernel: agent-scope (sc1) stores of the partial, every wave drains
+// them (vmcnt(0)) before the barrier and the counter increment, agent-scope loads by the last.
+constexpr int kAmGroup = 64;
+MG_DEVICE int am_groups(int G) { return (G + kAmGroup - 1) / kAmGroup; }
+
+// max key of n (<= 64 per pass) agent-scope partials per row b; wave w takes rows w, w + 4
+template <int B>
+MG_DEVICE void am_reduce(const unsigned long long* src, long ld, int n, unsigned long long (&out)[B],
+                         unsigned long long* sh) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int b = wid; b < B; b += 4) {
+    unsigned long long best = 0;
+    for (int i = lane; i < n; i += 64)
+      best = umax64(best, __hip_atomic_load(src + (long)b * ld + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    best = wave_umax64(best);
+    if (lane == 0) sh[b] = best;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < B; ++b) out[b] = sh[b];
+}
+
+template <int B>
+MG_DEVICE void gemv_argmax(const GemvArgmax& am, const unsigned long long (&key)[B], bool mine, int row) {
+  __shared__ unsigned long long kk[B][16];
+  __shared__ unsigned long long sh[B];
+  __shared__ int last;
+  if (mine) {  // this lane's best over the rows it produced (0: none)
+#pragma unroll
+    for (int b = 0; b < B; ++b) kk[b][row] = key[b];
+  }
+  __syncthreads();
+  const int G = gridDim.x, NG = am_groups(G);
+  const int grp = blockIdx.x / kAmGroup, gsize = min(kAmGroup, G - grp * kAmGroup);
+  unsigned long long* p1 = am.part;           // [B][G]
+  unsigned long long* p2 = am.part + (long)B * G;  // [B][NG]
+  if (threadIdx.x < B) {
+    unsigned long long best = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) best = umax64(best, kk[threadIdx.x][r]);
+    __hip_atomic_store(p1 + (long)threadIdx.x * G + blockIdx.x, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(am.cnt + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(gsize - 1);
+  __syncthreads();
+  if (!last) return;
+  // last of its group: the group's best -> level 2
+  unsigned long long best[B];
+  am_reduce<B>(p1 + (long)grp * kAmGroup, G, gsize, best, sh);
+  if (threadIdx.x < B)
+    __hip_atomic_store(p2 + (long)threadIdx.x * NG + grp, best[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(am.cnt + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = __hip_atomic_fetch_add(am.cnt + NG, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(NG - 1);
+  }
+  __syncthreads();
+  if (!last) return;
+  am_reduce<B>(p2, NG, NG, best, sh);
+  if (threadIdx.x == 0) {
+    const int pos = *am.pos;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const int64_t t = (int64_t)(0xffffffffu - (uint32_t)best[b]);
+      am.tok[b] = t;
+      if (am.seq) am.seq[(long)b * am.seq_ld + pos + 1] = t;
+    }
+    *am.pos = pos + 1;
+    __hip_atomic_store(am.cnt + NG, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <int B, int LPR>
 __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ x,
                                                    const bf16_t* __restrict__ W,
@@ -31,7 +132,8 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ x,
                                                    const bf16_t* __restrict__ bias,
                                                    const bf16_t* __restrict__ resid, int epi,
                                                    const bf16_t* __restrict__ lnw,
-                                                   const bf16_t* __restrict__ lnb, float eps) {
+                                                   const bf16_t* __restrict__ lnb, float eps,
+                                                   const GemvArgmax am) {
   extern __shared__ __attribute__((aligned(16))) bf16_t xs[];  // [B][K]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   constexpr int RPW = 64 / LPR;  // rows per wave
@@ -47,12 +149,64 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ x,
 #pragma unroll
     for (int u = 0; u < NPF; ++u) {
       const int c = j * 8 + u * STRIDE;
-      wpf[u] = c < K ? ld16(wr + c) : make_uint4(0, 0, 0, 0);
+      wpf[u] = c < K ? ld16_nt(wr + c) : make_uint4(0, 0, 0, 0);
     }
   }
   if (lnw) {
     // fused LayerNorm of the B input rows (wave w normalises rows w, w+4): the same lane/chunk
     // order and wave reduction as ln_fwd_kernel, so the staged bf16 rows equal its output
+    // K <= 1024 (GPT-2 small / medium): the row, gamma and beta chunks are loaded once into
+    // registers (one memory round trip instead of three dependent L2 reads); wider rows re-read
+    if (K <= 1024) {
+      for (int b = wid; b < B; b += 4) {
+        const bf16_t* xr = x + (long)b * K;
+        uint4 xv[2], wv[2], bv[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int c = lane * 8 + u * 512;
+          const bool ok = c < K;
+          xv[u] = ok ? ld16(xr + c) : make_uint4(0, 0, 0, 0);
+          wv[u] = ok ? ld16(lnw + c) : make_uint4(0, 0, 0, 0);
+          bv[u] = ok ? ld16(lnb + c) : make_uint4(0, 0, 0, 0);
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          float v[8];
+          unpack8(xv[u], v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s += v[e];  // zero chunks past K add nothing
+        }
+        const float mu = wave_sum(s) / K;
+        float ss = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if (lane * 8 + u * 512 < K) {
+            float v[8];
+            unpack8(xv[u], v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float d = v[e] - mu;
+              ss += d * d;
+            }
+          }
+        }
+        const float rs = rsqrtf(wave_sum(ss) / K + eps);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int c = lane * 8 + u * 512;
+          if (c < K) {
+            float v[8], wf[8], bf[8], o[8];
+            unpack8(xv[u], v);
+            unpack8(wv[u], wf);
+            unpack8(bv[u], bf);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = (v[e] - mu) * rs * wf[e] + bf[e];
+            st16(xs + b * K + c, pack8(o));
+          }
+        }
+      }
+    } else {
     for (int b = wid; b < B; b += 4) {
       const bf16_t* xr = x + (long)b * K;
       float s = 0.f;
@@ -84,6 +238,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ x,
         st16(xs + b * K + c, pack8(o));
       }
     }
+    }
   } else {
     for (int i = threadIdx.x * 8; i < B * K; i += 256 * 8) st16(xs + i, ld16(x + i));
   }
@@ -91,6 +246,25 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ x,
   // LPR lanes per output row: 16 (4 rows per wave) for wide outputs (the LM head), 64 (one row per
   // wave, the whole row's loads in flight at once) for the block projections, whose 48-192
   // workgroups at 16 lanes per row left most of the chip idle and the HBM latency exposed
+  auto epilogue = [&](float (&acc)[B], int n) {
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+#pragma unroll
+      for (int o = 1; o < LPR; o <<= 1) acc[b] += __shfl_xor(acc[b], o, 64);
+    }
+    if (n < N && j == 0) {
+      const float bv = bias ? bf2f(bias[n]) : 0.f;
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        float v = acc[b] + bv;
+        if (epi == 2) v = gelu_f(v);
+        if (epi == 3) v += bf2f(resid[(long)b * ldy + n]);
+        const bf16_t o = f2bf(v);
+        y[(long)b * ldy + n] = o;
+        acc[b] = bf2f(o);  // the argmax ranks the stored (bf16) logits
+      }
+    }
+  };
   float acc[B];
 #pragma unroll
   for (int b = 0; b < B; ++b) acc[b] = 0.f;
@@ -110,52 +284,64 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ x,
         }
       }
     }
-  } else if (n < N) {
-    const bf16_t* wr = W + (long)n * K;
-    int c = j * 8;
-    for (; c + 3 * STRIDE < K; c += 4 * STRIDE) {  // 4 loads in flight per lane
-      uint4 wv[4];
+    epilogue(acc, n);
+  } else {
+    // wide outputs: grid-stride over 16-row blocks (a few hundred workgroups stage x once each;
+    // the fused argmax then pays its cross-workgroup hand-off once per workgroup)
+    unsigned long long best[B];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) wv[u] = ld16(wr + c + u * STRIDE);
+    for (int b = 0; b < B; ++b) best[b] = 0ull;
+    // work items = (16-row block, 1024-column segment); the next item's 8 chunks per lane are
+    // requested before the current item's FMAs, so every lane keeps a full item in flight
+    const int nrb = (N + 15) / 16;
+    const int nseg = (K + 16 * 8 * 8 - 1) / (16 * 8 * 8);
+    const int nit = (blockIdx.x < nrb ? (nrb - 1 - blockIdx.x) / gridDim.x + 1 : 0) * nseg;
+    auto load_item = [&](int it, uint4 (&r)[8]) {
+      const int rb = blockIdx.x + (it / nseg) * gridDim.x, seg = it % nseg;
+      const int nr = min((rb * 4 + wid) * RPW + g, N - 1);
+      const bf16_t* wr = W + (long)nr * K + seg * 1024;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float wf[8];
-        unpack8(wv[u], wf);
+      for (int u = 0; u < 8; ++u) {
+        const int c = seg * 1024 + j * 8 + u * STRIDE;
+        r[u] = c < K ? ld16_nt(wr + j * 8 + u * STRIDE) : make_uint4(0, 0, 0, 0);
+      }
+    };
+    uint4 cur[8], nxt[8];
+    if (nit > 0) load_item(0, cur);
+    for (int it = 0; it < nit; ++it) {
+      if (it + 1 < nit) load_item(it + 1, nxt);
+      const int rb = blockIdx.x + (it / nseg) * gridDim.x, seg = it % nseg;
+      const int nr = (rb * 4 + wid) * RPW + g;
+      if (seg == 0) {
 #pragma unroll
-        for (int b = 0; b < B; ++b) {
-          float xf[8];
-          unpack8(ld16(xs + b * K + c + u * STRIDE), xf);
+        for (int b = 0; b < B; ++b) acc[b] = 0.f;
+      }
 #pragma unroll
-          for (int e = 0; e < 8; ++e) acc[b] = __builtin_fmaf(wf[e], xf[e], acc[b]);
+      for (int u = 0; u < 8; ++u) {
+        const int c = seg * 1024 + j * 8 + u * STRIDE;
+        if (c < K) {
+          float wf[8];
+          unpack8(cur[u], wf);
+#pragma unroll
+          for (int b = 0; b < B; ++b) {
+            float xf[8];
+            unpack8(ld16(xs + b * K + c), xf);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[b] = __builtin_fmaf(wf[e], xf[e], acc[b]);
+          }
         }
       }
-    }
-    for (; c < K; c += STRIDE) {
-      float wf[8];
-      unpack8(ld16(wr + c), wf);
+      if (seg == nseg - 1) {
+        epilogue(acc, nr);
+        if (am.part && nr < N && j == 0) {
 #pragma unroll
-      for (int b = 0; b < B; ++b) {
-        float xf[8];
-        unpack8(ld16(xs + b * K + c), xf);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[b] = __builtin_fmaf(wf[e], xf[e], acc[b]);
+          for (int b = 0; b < B; ++b) best[b] = umax64(best[b], amax_key(acc[b], nr));
+        }
       }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
     }
-  }
-#pragma unroll
-  for (int b = 0; b < B; ++b) {
-#pragma unroll
-    for (int o = 1; o < LPR; o <<= 1) acc[b] += __shfl_xor(acc[b], o, 64);
-  }
-  if (n < N && j == 0) {
-    const float bv = bias ? bf2f(bias[n]) : 0.f;
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-      float v = acc[b] + bv;
-      if (epi == 2) v = gelu_f(v);
-      if (epi == 3) v += bf2f(resid[(long)b * ldy + n]);
-      y[(long)b * ldy + n] = f2bf(v);
-    }
+    if (am.part) gemv_argmax<B>(am, best, j == 0, wid * RPW + g);
   }
 }
 
@@ -165,20 +351,39 @@ namespace mg {
 
 bool gemv_supported(int B, int K) { return B >= 1 && B <= kGemvMaxB && K % 8 == 0 && K <= kGemvMaxK; }
 
+// wide outputs: a few workgroups per CU, grid-striding over the 16-row blocks
+int gemv_wide_cap() {
+  static int cap = 0;
+  if (!cap) {
+    const char* e = getenv("MINGPT_GEMV_WIDE_GRID");
+    cap = e ? atoi(e) : 512;
+    if (cap <= 0) cap = 512;
+  }
+  return cap;
+}
+int gemv_grid(int N) { return N > 8192 ? min(cdiv(N, 16), gemv_wide_cap()) : cdiv(N, 4); }
+// argmax workspace: 8-byte partials per (row, workgroup) and per (row, group), counters per group + 1
+size_t gemv_argmax_part_words(int B, int N) {
+  const int G = gemv_grid(N);
+  return (size_t)B * (G + (G + kAmGroup - 1) / kAmGroup);
+}
+size_t gemv_argmax_counters(int N) { return (gemv_grid(N) + kAmGroup - 1) / kAmGroup + 1; }
+
 void gemv(const bf16_t* x, const bf16_t* W, bf16_t* y, int B, int N, int K, long ldy, const bf16_t* bias,
           const bf16_t* resid, int epi, hipStream_t stream, const bf16_t* lnw, const bf16_t* lnb,
-          float eps) {
+          float eps, const GemvArgmax* am) {
   const size_t smem = sizeof(bf16_t) * (size_t)B * K;
   // one row per wave (N / 4 workgroups) up to ~8k outputs; 4 rows per wave beyond (the LM head
   // already launches thousands of workgroups and re-stages x in each)
   const bool wide = N > 8192;
-  const int grid = wide ? cdiv(N, 16) : cdiv(N, 4);
-#define MG_GEMV_CASE(b)                                                                                   \
-  case b:                                                                                                 \
-    if (wide)                                                                                             \
-      gemv_kernel<b, 16><<<grid, 256, smem, stream>>>(x, W, y, N, K, ldy, bias, resid, epi, lnw, lnb, eps); \
-    else                                                                                                  \
-      gemv_kernel<b, 64><<<grid, 256, smem, stream>>>(x, W, y, N, K, ldy, bias, resid, epi, lnw, lnb, eps); \
+  const int grid = gemv_grid(N);
+  const GemvArgmax amv = am ? *am : GemvArgmax{nullptr, nullptr, nullptr, nullptr, 0, nullptr};
+#define MG_GEMV_CASE(b)                                                                                        \
+  case b:                                                                                                      \
+    if (wide)                                                                                                  \
+      gemv_kernel<b, 16><<<grid, 256, smem, stream>>>(x, W, y, N, K, ldy, bias, resid, epi, lnw, lnb, eps, amv); \
+    else                                                                                                       \
+      gemv_kernel<b, 64><<<grid, 256, smem, stream>>>(x, W, y, N, K, ldy, bias, resid, epi, lnw, lnb, eps, amv); \
     break;
   switch (B) {  // exact row counts: the kernel stages and writes exactly B rows
     MG_GEMV_CASE(1) MG_GEMV_CASE(2) MG_GEMV_CASE(3) MG_GEMV_CASE(4)

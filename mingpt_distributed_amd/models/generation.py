@@ -109,6 +109,11 @@ def bf16_weights(model):
 
 
 class _GpuCache:
+    """KV caches ([B, Tmax, 3D] qkv rows per layer) plus the captured decode steps of one model at
+    one batch size.  Kept on the model across ``generate`` calls (``_gpu_cache``): a later call
+    with the same batch re-prefills into the same buffers and replays the same hipGraphs, unless
+    a weight changed storage or version since the capture (then the graphs are re-captured)."""
+
     def __init__(self, model, idx, tmax):
         from ..ops._ext import ext
         from ..ops import gemm as G
@@ -120,13 +125,21 @@ class _GpuCache:
         B, T = idx.shape
         cfg = model.config
         D = cfg.n_embed
+        self.B = B
         self.caches = [torch.empty(B, tmax, 3 * D, device=idx.device, dtype=torch.bfloat16)
                        for _ in range(cfg.n_layer)]
+        self.stamp = _weight_stamp(model)
         self.logits = self._run(idx, 0)
 
-    def _run(self, idx, pos0, pos_dev=None):
+    def prefill(self, idx):
+        self.logits = self._run(idx, 0)
+        return self.logits
+
+    def _run(self, idx, pos0, pos_dev=None, greedy=None):
         """Prefill (pos0 == 0) or one decode step at position pos0 (or at ``pos_dev[0]``, an int32
-        device scalar, when captured in a hipGraph)."""
+        device scalar, when captured in a hipGraph).  ``greedy`` = (tok [B] int64, pos_dev,
+        seq [B, Tmax + 1] int64): the LM-head kernel also takes the argmax, writes it to tok and
+        seq[:, pos + 1] and advances pos_dev -- the step then needs nothing from the host."""
         C, G, bf = self.C, self.G, self.bf
         m = self.model
         tr, cfg = m.transformer, m.config
@@ -135,19 +148,22 @@ class _GpuCache:
         wpe = bf(tr.wpe.weight)
         if pos0 == 0:
             x = C.embedding_fwd(idx.contiguous(), bf(tr.wte.weight), wpe, 0.0, 0).view(B * T, D)
+        elif pos_dev is not None:  # the position row is picked on the device (one kernel)
+            x = C.embedding_fwd(idx.contiguous(), bf(tr.wte.weight), wpe, 0.0, 0, pos_dev).view(B * T, D)
         else:  # single token at position pos0
-            wrow = wpe.index_select(0, pos_dev) if pos_dev is not None else wpe[pos0:pos0 + 1].contiguous()
-            x = C.embedding_fwd(idx.contiguous(), bf(tr.wte.weight), wrow, 0.0, 0).view(B * T, D)
+            x = C.embedding_fwd(idx.contiguous(), bf(tr.wte.weight), wpe[pos0:pos0 + 1], 0.0, 0).view(B * T, D)
         # decode rows (B <= 8) go through the skinny GEMM (gemv.hip): at M = B the MFMA GEMM has
         # one row tile and walks K latency-bound; prefill uses the MFMA GEMM
         skinny = pos0 > 0 and C.gemv_supported(B * T, 4 * D)
 
-        def lin(inp, w, b, epi, resid=None, ld=0, ln=None):
+        def lin(inp, w, b, epi, resid=None, ld=0, ln=None, am=None):
             """epi(LN(inp) @ w^T + b) with ``ln`` = a LayerNorm module applied first (fused into
             the skinny GEMM's staging at decode time)."""
             if skinny:
                 code = {"none": 0, "bias": 1, "gelu": 2, "resid": 3}[epi]
                 lw, lb = (bf(ln.weight), bf(ln.bias)) if ln is not None else (None, None)
+                if am is not None:
+                    return C.gemv(inp, bf(w), code, None, None, ld, lw, lb, eps, am[0], am[1], am[2])
                 return C.gemv(inp, bf(w), code, bf(b) if b is not None else None, resid, ld, lw, lb, eps)
             if ln is not None:
                 inp, _, _ = C.layernorm_fwd(inp, bf(ln.weight), bf(ln.bias), eps)
@@ -170,15 +186,32 @@ class _GpuCache:
             x = lin(u, mm.c_proj.weight, mm.c_proj.bias, "resid", resid=x)
         last = x.view(B, T, D)[:, -1].contiguous()
         V = cfg.vocab_size
-        logits = lin(last, m.lm_head.weight, None, "none", ld=(V + 7) // 8 * 8, ln=tr.ln_f)
+        am = None
+        if greedy is not None and skinny and V > 8192:
+            am = (greedy[0].view(B), greedy[1], greedy[2])
+        logits = lin(last, m.lm_head.weight, None, "none", ld=(V + 7) // 8 * 8, ln=tr.ln_f, am=am)
+        if greedy is not None and am is None:  # small vocab (no fused argmax): same effect in torch
+            tok, pd, seq = greedy
+            nxt = logits[:, :V].argmax(-1)
+            tok.view(B).copy_(nxt)
+            seq.index_copy_(1, (pd.long() + 1), nxt.view(B, 1))
+            pd.add_(1)
         return logits[:, :V]
 
+    def _fresh(self):
+        st = _weight_stamp(self.model)
+        if st != self.stamp:  # a weight moved or changed: captured pointers / bf16 copies are stale
+            self.stamp = st
+            self.__dict__.pop("_graph", None)
+            self.__dict__.pop("_ggraph", None)
+
     def step(self, tok, pos):
-        """One decode step.  Decoding is launch-bound (B rows through ~10 kernels per layer), so
+        """One decode step.  Decoding is launch-bound (B rows through ~5 kernels per layer), so
         the step is captured once as a hipGraph over static token / position buffers and
         replayed; the KV caches are persistent buffers the captured kernels append to."""
         if not _GRAPH_DECODE:
             return self._run(tok, pos)
+        self._fresh()
         g = getattr(self, "_graph", None)
         if g is None:
             g = self._graph = {"tok": tok.clone(), "pos": torch.full((1,), pos, dtype=torch.int32,
@@ -192,6 +225,50 @@ class _GpuCache:
         g["pos"].fill_(pos)
         g["graph"].replay()
         return g["logits"]
+
+    def greedy(self, tok, pos, n):
+        """n greedy decode steps starting with token ``tok`` [B, 1] at position ``pos``: the captured
+        step takes its input token and position from device buffers that its own LM-head kernel
+        overwrites (fused argmax), so the n replays are queued back to back without a host round
+        trip.  Returns the n new tokens [B, n] (positions pos + 1 .. pos + n)."""
+        assert pos + n <= self.tmax
+        B = tok.shape[0]
+        self._fresh()
+        g = getattr(self, "_ggraph", None)
+        if g is None:
+            dev = tok.device
+            g = {"tok": tok.clone(), "pos": torch.full((1,), pos, dtype=torch.int32, device=dev),
+                 "seq": torch.zeros(B, self.tmax + 1, dtype=torch.long, device=dev)}
+            self._run(g["tok"], max(pos, 1), g["pos"], (g["tok"], g["pos"], g["seq"]))  # warm-up:
+            self._ggraph = g  # workspaces are allocated outside the capture
+        if _GRAPH_DECODE and "graph" not in g:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                self._run(g["tok"], max(pos, 1), g["pos"], (g["tok"], g["pos"], g["seq"]))
+            g["graph"] = graph
+        g["tok"].copy_(tok)
+        g["pos"].fill_(pos)
+        for _ in range(n):
+            if _GRAPH_DECODE:
+                g["graph"].replay()
+            else:
+                self._run(g["tok"], max(pos, 1), g["pos"], (g["tok"], g["pos"], g["seq"]))
+        return g["seq"][:, pos + 1:pos + 1 + n]
+
+
+def _weight_stamp(model):
+    return tuple((p.data_ptr(), p._version) for p in model.parameters())
+
+
+def _gpu_cache(model, idx, tmax):
+    """The model's decode state for this batch size (re-prefilled), or a new one."""
+    c = model.__dict__.get("_mg_decode_cache")
+    if c is not None and c.B == idx.size(0) and c.tmax == tmax and c.caches[0].device == idx.device:
+        c.prefill(idx)
+        return c
+    c = _GpuCache(model, idx, tmax)
+    model.__dict__["_mg_decode_cache"] = c
+    return c
 
 
 _GRAPH_DECODE = True  # set False to launch the decode step eagerly
@@ -207,12 +284,14 @@ def generate(model, idx, max_new_tokens: int, temperature: float = 1.0, do_sampl
             logits, _ = model(idx_cond)
             idx = torch.cat((idx, _sample(logits[:, -1, :], temperature, do_sample, top_k)), dim=1)
         return idx
+    if idx.is_cuda and not do_sample and max_new_tokens > 0:
+        return _generate_greedy_gpu(model, idx, max_new_tokens)
     cache = None
     for _ in range(max_new_tokens):
         T = idx.size(1)
         if cache is None or T > bs:
             idx_cond = idx if T <= bs else idx[:, -bs:]
-            cache = _GpuCache(model, idx_cond, bs) if idx.is_cuda else _CpuCache(model, idx_cond)
+            cache = _gpu_cache(model, idx_cond, bs) if idx.is_cuda else _CpuCache(model, idx_cond)
             cache.pos = idx_cond.size(1)
             logits = cache.logits
         idx_next = _sample(logits, temperature, do_sample, top_k)
@@ -223,3 +302,26 @@ def generate(model, idx, max_new_tokens: int, temperature: float = 1.0, do_sampl
         logits = cache.step(idx_next, cache.pos)
         cache.pos += 1
     return idx
+
+
+def _generate_greedy_gpu(model, idx, max_new_tokens):
+    """Greedy decode on the GPU: one prefill per context window, then the device-side token loop
+    (``_GpuCache.greedy``) for every position the window still has room for.  Once the sequence
+    outgrows block_size, each token is a fresh prefill of the last block_size tokens -- the
+    reference's crop-every-step semantics (``/root/reference/mingpt/model.py:333``)."""
+    bs = model.block_size
+    B, T0 = idx.shape
+    out = torch.empty(B, T0 + max_new_tokens, dtype=torch.long, device=idx.device)
+    out[:, :T0] = idx
+    T, end = T0, T0 + max_new_tokens
+    while T < end:
+        ctx = out[:, max(0, T - bs):T]
+        L = ctx.size(1)
+        cache = _gpu_cache(model, ctx, bs)
+        out[:, T] = cache.logits.argmax(-1)
+        T += 1
+        n = min(end - T, bs - L)
+        if n > 0:
+            out[:, T:T + n] = cache.greedy(out[:, T - 1:T], L, n)
+            T += n
+    return out

@@ -107,6 +107,31 @@ def test_generate_graph_decode_matches_eager(monkeypatch):
     assert c.shape == (3, 87)
 
 
+def test_greedy_device_loop_matches_host_argmax():
+    """The device-side greedy loop (LM-head GEMV with the fused argmax writing the next token and
+    position) == the logits step followed by torch.argmax, token for token; vocab > 8192 takes
+    the fused path.  Also: generate() across the block_size window and a second call that reuses
+    the cached decode state."""
+    from mingpt_distributed_amd.models import generation as gen
+
+    torch.manual_seed(0)
+    model = GPT(_cfg(vocab_size=9000, block_size=64), verbose=False).cuda().to(torch.bfloat16).eval()
+    B, T0, n = 2, 5, 30
+    idx = torch.randint(0, 9000, (B, T0), device="cuda")
+    with torch.no_grad():
+        ref = gen._GpuCache(model, idx, 64)
+        toks = [ref.logits.argmax(-1)]
+        for k in range(n):
+            toks.append(ref.step(toks[-1].view(B, 1), T0 + k).argmax(-1))
+        dev = gen._GpuCache(model, idx, 64)
+        seq = dev.greedy(dev.logits.argmax(-1).view(B, 1), T0, n)
+    assert torch.equal(seq, torch.stack(toks[1:], 1)), (seq, torch.stack(toks[1:], 1))
+    a = model.generate(idx, 90, do_sample=False)  # device loop to position 63, then sliding prefills
+    b = model.generate(idx, 90, do_sample=False)  # reuses the cached state and graphs
+    assert a.shape == (B, T0 + 90) and torch.equal(a, b)
+    assert torch.equal(a[:, T0:T0 + n + 1], torch.stack(toks, 1))
+
+
 def test_gpt2_shape_step():
     """Full GPT-2 layer shapes (D=768, H=12, hd=64) at a short sequence through the engine."""
     torch.manual_seed(0)
