@@ -109,51 +109,15 @@ MG_DEVICE float block_max(float v, float* red) {
   return t;
 }
 
-// ---------------------------------------------------------------- Philox-4x32-10 RNG
-// Counter-based: the dropout mask of element e under seed s is a pure function of (s, e), so
-// the backward pass regenerates it instead of storing it.
-MG_DEVICE uint4 philox4x32(uint4 ctr, uint2 key) {
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    const uint32_t lo0 = ctr.x * 0xD2511F53u, hi0 = __umulhi(ctr.x, 0xD2511F53u);
-    const uint32_t lo1 = ctr.z * 0xCD9E8D57u, hi1 = __umulhi(ctr.z, 0xCD9E8D57u);
-    ctr = make_uint4(hi1 ^ ctr.y ^ key.x, lo1, hi0 ^ ctr.w ^ key.y, lo0);
-    key.x += 0x9E3779B9u;
-    key.y += 0xBB67AE85u;
-  }
-  return ctr;
-}
-
-// 4 random words for the aligned group of 4 elements starting at e4*4.
-MG_DEVICE uint4 rand4(uint64_t seed, uint64_t e4) {
-  return philox4x32(make_uint4((uint32_t)e4, (uint32_t)(e4 >> 32), 0x5eed5eedu, 0u),
-                    make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
-}
-
-// keep-threshold: keep element iff rand >= thr, thr = p * 2^32.
-inline uint32_t dropout_threshold(float p) {
-  double t = (double)p * 4294967296.0;
-  if (t >= 4294967295.0) return 0xffffffffu;
-  return (uint32_t)t;
-}
-
-// Apply dropout to 8 consecutive elements starting at e (e % 8 == 0).
-MG_DEVICE void dropout8(float (&v)[8], uint64_t seed, uint64_t e, uint32_t thr, float scale) {
-  const uint4 r0 = rand4(seed, e >> 2), r1 = rand4(seed, (e >> 2) + 1);
-  const uint32_t r[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-#pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = (r[i] >= thr) ? v[i] * scale : 0.f;
-}
-
 // ---------------------------------------------------------------- residual-stream dropout mask
 // 8-bit decisions (keep iff byte >= thr8, thr8 = round(256 p), scale 256 / (256 - thr8): the same
 // quantised p as the attention dropout).  Element (m, n) of a row-major [M, N] tensor takes byte
 // (n & 3) of the word  fmix32(m * ceil(N / 4) + (n >> 2) + key(seed))  (32-bit index arithmetic:
 // exact below 2^32 words, i.e. 16 G elements per tensor).  One word per 4 consecutive elements:
 // a GEMM epilogue lane holding C[m][n..n+3] draws exactly one, a thread owning 8 consecutive
-// elements two.  The murmur3 finaliser is 2 multiplies per word; the Philox-4x32-10 call this
-// replaced cost 40 quarter-rate multiplies per 16 decisions and made the standalone dropout-
-// backward kernels RNG-bound (each of their threads used one word of two calls).
+// elements two.  The murmur3 finaliser is 2 multiplies per word (a Philox-4x32-10 generator, used
+// in round 1, cost 40 quarter-rate multiplies per 16 decisions and made the standalone dropout-
+// backward kernels RNG-bound).  Counter-based: backward regenerates the mask, nothing is stored.
 constexpr uint32_t kRowDropSalt = 0x0d0f0d0fu;
 
 inline uint32_t dropout_threshold8(float p) {

@@ -1,147 +1,18 @@
-// Causal flash attention, forward and backward, for gfx950 (CDNA4, MI355X).
+// Decode attention for gfx950 (CDNA4, MI355X): one new query per sequence against the KV cache.
 //
-// Replaces the reference's nn.MultiheadAttention math path
-// (/root/reference/mingpt/model.py:147-165: in-proj split, q*scale, baddbmm with the [T,T] mask,
-// softmax, dropout, bmm PV, plus the discarded head-averaged weights) with a true causal kernel
-// that never materialises [T, T] (fixes D4: the reference's additive 0/1 mask was not causal).
-//
-// I/O layout: qkv [B*T, 3*D] bf16 straight from the c_attn GEMM (q | k | v, head h at columns
-// h*hd..), out [B*T, D] bf16, lse [B*H*T] fp32 (log2 domain).  hd <= 64 (every GPT-2 size is 64;
-// gpt-mini/micro are 32, gpt-nano 16): tiles are 64 wide and zero-padded.
-//
-// Forward (FA2 structure, MI355X mapping):
-//  * workgroup = 4 waves = 128 queries of one (b, h); each wave owns 32 queries.
-//  * Q fragments live in VGPRs for the whole kernel; K/V tiles of 64 keys are staged through LDS
-//    (double buffer, loads for tile t+1 issued before the MFMAs of tile t).
-//  * S^T = K Q^T with v_mfma_f32_32x32x16_bf16 ("swapped" operands): the query is on the lane,
-//    so the softmax row statistics are lane-local (one xor-32 shuffle joins the two halves).
-//  * P is converted to bf16 in registers and used directly as the B operand of O^T = V^T P^T
-//    (guide §3 "accumulator tile as the next MFMA's operand"); V^T fragments come from LDS with
-//    ds_read_b64_tr_b16 in the matching permuted key order.  O^T keeps queries on the lane too,
-//    so the online-softmax rescale is a per-lane multiply.
-//  * LDS images use a 128-B-row XOR swizzle that is bank-conflict-free for both the row reads
-//    (ds_read_b128) and the transposed reads (found by exhaustive search, see PERF.md).
-//  * heaviest (last) query blocks are launched first; fully-masked K tiles are skipped per wave.
-//
-// Backward (key-block parallel):
-//  * workgroup = 4 waves = 128 keys of one (b, h); each wave keeps its 32 keys' K and V fragments
-//    in VGPRs and dK^T/dV^T accumulators (keys on the lane) across the whole query sweep.
-//  * per 64-query tile (Q, dO, lse, delta staged in LDS): S and dP with the key on the lane, P and
-//    dS in registers feed dV^T += dO^T P and dK^T += Q^T dS directly (tr-reads of Q/dO);
-//    dS is transposed once through LDS for dQ = dS K, the 4 waves' dQ partials are summed with
-//    LDS float atomics, then one fp32 global atomic per element per workgroup.
-//  * attention dropout: Philox mask regenerated from (seed, b, h, q, key) in both passes.
-#include "common.h"
+// The reference re-runs the full forward over the whole prefix for every generated token
+// (/root/reference/mingpt/model.py:322-356); models/generation.py keeps each layer's qkv rows as a
+// cache instead and this kernel attends the new token's query to them (training attention:
+// attention_train.hip).  Tried and measured slower at GPT-2 decode shapes (B=1, L <= 288): all of
+// a key row's chunks requested at once (registers), and a 256-thread fold of the key groups
+// (extra barriers) -- 5.3 -> 5.8 us per call.
+#include "attn_common.h"
 #include "kernels.h"
 
 using namespace mg;
+using mg::attn::fexp2;
 
 namespace {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-
-constexpr int HD = 64;        // tile head dim
-constexpr int ROWB = HD * 2;  // 128-B LDS rows
-constexpr float kNegBig = -1e30f;
-
-// conflict-free for ds_read_b128 (32-row operand) and both ds_read_b64_tr_b16 patterns
-MG_DEVICE int swz(int r) { return ((r >> 1) & 3) | ((((r >> 1) ^ (r >> 3)) & 1) << 2); }
-MG_DEVICE int lds_off(int row, int ch) { return row * ROWB + ((ch ^ swz(row)) << 4); }
-
-struct AttnArgs {
-  const bf16_t* qkv;
-  bf16_t* out;
-  float* lse;          // [B*H*T], log2 domain
-  const bf16_t* dout;  // bwd
-  const float* delta;  // bwd [B*H*T]
-  float* dq;           // bwd fp32 dQ: [B*T, D] atomic accumulator, or per-key-block partials
-  long dq_part;        // bwd256: elements between key-block partials of dq (plain stores)
-  bf16_t* dqkv;        // bwd [B*T, 3D]
-  uint32_t* dmask;     // dropout keep-bits [B*H][2*ceil(T/64)][T] (attention_train.hip writes, bwd reads)
-  int B, T, H, hd, D;
-  float scale_log2;    // log2(e) / sqrt(hd)
-  uint64_t seed;
-  uint32_t seed_key;   // fwd dropout hash key derived from seed
-  const uint64_t* sofs;  // hipGraph mode: seed_key is derived on the device (common.h eff_seed)
-  uint32_t thr;        // 8-bit keep threshold: keep iff random byte >= thr (0 = no dropout)
-  float dscale;        // 1 / (1 - thr/256)
-  uint32_t kadd;       // SWAR keep test: 4 x (128 - thr) if thr <= 128, else 4 x (256 - thr)
-};
-
-MG_DEVICE float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }  // v_exp_f32, no denorm fixup
-
-// 32-bit avalanche mixer (xorshift-multiply, "lowbias32" constants): a bijection with good
-// avalanche, 5 VALU ops; the attention-dropout bytes are mix32 of distinct counters.
-MG_DEVICE uint32_t mix32(uint32_t x) {
-  x ^= x >> 16;
-  x *= 0x7feb352du;
-  x ^= x >> 15;
-  x *= 0x846ca68bu;
-  x ^= x >> 16;
-  return x;
-}
-
-MG_DEVICE bf16x8 lds_row_frag(const char* base, int row, int ch) {
-  return *reinterpret_cast<const bf16x8*>(base + lds_off(row, ch));
-}
-
-// Transposed 8-element fragment: column col of rows r0..r0+3 (elements 0..3) and r1..r1+3 (4..7).
-// Lane (in its 16-lane group) 4q+p addresses row r?+q, columns colbase+4p..+3.
-MG_DEVICE bf16x8 lds_tr_frag(const char* base, int r0, int r1, int colbase, int lane) {
-  const int i = lane & 15, q = i >> 2, p = i & 3;
-  const int col = colbase + 4 * p;
-  const int ra = r0 + q, rb = r1 + q;
-  const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_s16x4*)(base + lds_off(ra, col >> 3) + (col & 7) * 2));
-  const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_s16x4*)(base + lds_off(rb, col >> 3) + (col & 7) * 2));
-  const s16x8 v = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-// Byte offset of a transposed-read lane address (row, column) in an lds_off image.
-MG_DEVICE int tr_off(int row, int col) { return lds_off(row, col >> 3) + (col & 7) * 2; }
-
-// Transposed fragment from two precomputed per-lane offsets (rows r0+q and r0+8+q, or +4): the
-// swizzle is periodic in the row with period 16, so a 16-row-aligned row base is a plain byte
-// offset the caller passes as a compile-time constant (it lands in the ds_read offset field)
-// instead of a per-read swizzle computation.
-MG_DEVICE bf16x8 lds_tr_at(const char* base, int oa, int ob) {
-  const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + oa));
-  const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + ob));
-  const s16x8 v = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-MG_DEVICE bf16x8 lds_row_at(const char* base, int o) { return *reinterpret_cast<const bf16x8*>(base + o); }
-
-MG_DEVICE bf16x8 pack_frag(const f32x16& a, int s) {
-  s16x8 v;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(a[8 * s + j]);
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-// stage a [64 rows][64 cols] bf16 tile (rows r0.., column offset col0 in a row-major matrix with
-// leading dimension ld) into registers: 512 chunks of 16 B, 2 per thread.
-MG_DEVICE void load64(uint4 (&reg)[2], const bf16_t* base, long ld, int r0, int rows, int hd) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int idx = threadIdx.x + 256 * i;
-    const int row = idx >> 3, ch = idx & 7;
-    const int r = r0 + row;
-    reg[i] = (r < rows && ch * 8 < hd) ? ld16(base + (long)r * ld + ch * 8) : make_uint4(0, 0, 0, 0);
-  }
-}
-
-MG_DEVICE void store64(char* lds, const uint4 (&reg)[2]) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int idx = threadIdx.x + 256 * i;
-    *reinterpret_cast<uint4*>(lds + lds_off(idx >> 3, idx & 7)) = reg[i];
-  }
-}
 
 // =============================================================================== decode
 // One new query per sequence attending to a KV cache held as qkv rows [B, Tmax, 3D] (the prefill
