@@ -1,0 +1,43 @@
+#!/usr/bin/env python
+"""The GEMMs the default step routes to hipBLASLt (B=64 GPT-2, M = 65536 tokens), each through
+torch.mm (hipBLASLt) and through gemm.hip under every tile config (gemm_set_variant): qkv forward
+(bias), the plain data gradients (as NT against the transposed weight, as ops/gemm.gemm_dgrad
+runs them), LM-head forward and data gradient.  One JSON line per shape."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from bench.bench_epilogue import timeit
+from mingpt_distributed_amd.ops import gemm as G
+from mingpt_distributed_amd.ops._ext import ext
+
+M, D, V = int(os.environ.get("TOKENS", "65536")), 768, 50304
+r = lambda *s: torch.randn(*s, device="cuda").to(torch.bfloat16)
+C = ext()
+names = {0: "auto", 1: "T128", 2: "T256", 3: "T2x1", 4: "PP", 5: "W4", 6: "W4_192"}
+x, wq, bq = r(M, D), r(3 * D, D), r(3 * D)
+shapes = [("qkv_fwd_bias", M, 3 * D, D, lambda: torch.addmm(bq, x, wq.t()), lambda: G.gemm_nt(x, wq, bias=bq, epi="bias"))]
+for nm, n_in, n_out in (("proj_dgrad", D, D), ("fc_dgrad", D, 4 * D), ("qkv_dgrad", D, 3 * D)):
+    dy, w = r(M, n_out), r(n_out, n_in)
+    wt = w.t().contiguous()
+    shapes.append((nm, M, n_in, n_out, (lambda dy=dy, w=w: torch.mm(dy, w)), (lambda dy=dy, wt=wt: G.gemm_nt(dy, wt))))
+h, wl = r(M, D), r(V, D)
+shapes.append(("lmhead_fwd", M, V, D, lambda: torch.mm(h, wl.t()), lambda: G.gemm_nt(h, wl, ld=V)))
+dl, wlt = r(M, V), wl.t().contiguous()
+shapes.append(("lmhead_dgrad", M, D, V, lambda: torch.mm(dl, wl), lambda: G.gemm_nt(dl, wlt)))
+for nm, m, n, k, blas, ours in shapes:
+    fl = 2.0 * m * n * k
+    t = timeit(blas)
+    out = {"hipblaslt": [round(t * 1e3, 1), round(fl / t / 1e9)]}
+    for v in (0, 1, 2, 4, 5, 6):
+        C.gemm_set_variant(v)
+        try:
+            t = timeit(ours)
+            out[names[v]] = [round(t * 1e3, 1), round(fl / t / 1e9)]
+        except Exception as e:
+            out[names[v]] = str(e)[:50]
+    C.gemm_set_variant(0)
+    print(json.dumps({"shape": nm, "M": m, "N": n, "K": k, "us_tflops": out}), flush=True)

@@ -4,16 +4,18 @@ Granularity is chosen for the MI355X, not for module boundaries: one Function pe
 block (LN1 -> QKV GEMM+bias -> flash attention -> proj GEMM with fused bias+dropout+residual ->
 LN2 -> FC GEMM with fused bias+GELU -> proj GEMM with fused bias+dropout+residual), one for the
 embedding and one for final-LN + LM head + cross-entropy.  Every norm, attention, loss and
-elementwise op, every GEMM with a fused epilogue (bias+GELU, bias+dropout+residual, GELU', and all
-weight gradients with their fp32 accumulation) is a hand-written HIP kernel.  The GEMMs with
-nothing to fuse -- the qkv projection (bias only), the three plain data gradients of a block and
-the LM head's forward and data gradient -- run on the library GEMM (hipBLASLt through torch.mm)
-once they are large (``_big``), as the project brief allows for plain library GEMMs: at those
-shapes hipBLASLt's main loop was 5-25 % faster than the W4 kernel (PERF.md).  ``MINGPT_QKV_BLAS=0
-MINGPT_DGRAD_BLAS=0 MINGPT_LMHEAD_BLAS=0`` puts every GEMM on gemm.hip (the all-HIP path, also
-tested and benchmarked).  Weight gradients are accumulated in fp32 straight into
-``param.main_grad`` (see ``grads.py``) so the data-parallel engine can all-reduce a bucket the
-moment its last gradient lands.
+elementwise op and every GEMM of a transformer block (the fused-epilogue ones -- bias+GELU,
+bias+dropout+residual, GELU', the weight gradients with their fp32 accumulation -- and the plain
+ones: the qkv projection and the three data gradients) is a hand-written HIP kernel; so are the
+LM head's weight and data gradients.  One GEMM runs on the library (hipBLASLt through torch.mm):
+the LM head's forward ([M, 768] x [768, 50304], 6.6 GB of logits written at K = 768), where
+hipBLASLt is 1.7 % of the B=64 step faster than the W4 kernel (one-box A/B, PERF.md), as the
+project brief allows for plain library GEMMs.  ``MINGPT_LMHEAD_BLAS=0`` puts it on gemm.hip too
+(the all-HIP path, also tested and benchmarked); ``MINGPT_QKV_BLAS=1 MINGPT_DGRAD_BLAS=1
+MINGPT_LMHEAD_DGRAD_BLAS=1`` restores round 1's library routing of the plain block GEMMs, which
+measured equal in the step once the W4 main loop improved.  Weight gradients are accumulated in
+fp32 straight into ``param.main_grad`` (see ``grads.py``) so the data-parallel engine can
+all-reduce a bucket the moment its last gradient lands.
 
 Reference anchors: block structure ``/root/reference/mingpt/model.py:171-189`` (with D4/D5/D6
 fixed), embedding ``model.py:193-231``, head + loss ``model.py:309-320``.
@@ -40,16 +42,17 @@ def _bf16(t: torch.Tensor) -> torch.Tensor:
 
 # ------------------------------------------------------------------------------------ embedding
 
-# Plain GEMMs of the block (no fused epilogue) run on the library GEMM (hipBLASLt via torch.mm /
-# torch.addmm): the three epilogue-free data gradients (qkv, attention projection, MLP fc) and the
-# qkv projection, whose bias epilogue hipBLASLt fuses too.  One-box A/B at B=64: +1.0 % for the
-# dgrads, +0.5 % for qkv, +1.7 % together (920k -> 935k tok/s); hipBLASLt's main loop is ~20 %
-# faster than W4's at K >= 1536 (bench/gemm_ksweep.py) and these GEMMs have nothing to fuse.  The
-# weight gradients stay on gemm.hip (fp32 accumulate; the fp32-out library GEMM + add was 13 %
-# slower per step), as do the GELU / residual-dropout / GELU' epilogue GEMMs.
-_DGRAD_BLAS = os.environ.get("MINGPT_DGRAD_BLAS", "1") == "1"
+# Plain GEMMs of the block (no fused epilogue): the three epilogue-free data gradients (qkv,
+# attention projection, MLP fc) and the qkv projection (bias only) run on gemm.hip by default.
+# Round 1 routed them to hipBLASLt (+1.7 % then); after the W4 main-loop work the HIP kernels are
+# as fast or faster on these shapes (bench/gemm_blas_shapes.py: qkv 220 vs 248 us, fc dgrad 240
+# vs 266, qkv dgrad 178 vs 192, proj dgrad 80 vs 82) and the step A/B is equal (999.5k both,
+# profiles/round2_gemm_routing_ab.txt).  MINGPT_{DGRAD,QKV}_BLAS=1 restores the library routing.
+# The weight gradients stay on gemm.hip (fp32 accumulate; the fp32-out library GEMM + add was
+# 13 % slower per step).
+_DGRAD_BLAS = os.environ.get("MINGPT_DGRAD_BLAS", "0") == "1"
 _WGRAD_BLAS = os.environ.get("MINGPT_WGRAD_BLAS", "0") == "1"
-_QKV_BLAS = os.environ.get("MINGPT_QKV_BLAS", "1") == "1"
+_QKV_BLAS = os.environ.get("MINGPT_QKV_BLAS", "0") == "1"
 
 
 # Library calls cost more host time per launch than the extension's; small models (gpt-mini:
@@ -181,12 +184,15 @@ class TransformerBlockFn(_EngineFn):
 
 
 # ------------------------------------------------------------------------------------ head + loss
-# The LM head's forward and data-gradient GEMMs carry no epilogue (plain [M, 768] x [768, 50304]
-# and [M, 50304] x [50304, 768]): they go to the library GEMM (hipBLASLt via torch.mm), which beat
-# the hand-written W4 kernel on exactly these two shapes by 2.3 ms per B=64 step (one-box A/B,
-# PERF.md).  The weight gradient (fp32 accumulate into main_grad) and every fused GEMM stay on the
-# HIP kernels.  MINGPT_LMHEAD_BLAS=0 routes the head through gemm.hip as well.
+# The LM head's forward carries no epilogue (plain [M, 768] x [768, 50304], K = 768, 6.6 GB of
+# logits written): it goes to the library GEMM (hipBLASLt via torch.mm against a zero-padded
+# weight copy), 4.1 vs 5.0 ms per call on the W4 kernel (bench/gemm_blas_shapes.py) -- 1.7 % of the
+# step.  Its data gradient ([M, 50304] x [50304, 768], K = 50304) runs on gemm.hip (the 128x96-wave
+# W4 tile: 3.75 vs 3.81 ms), the weight gradient too (fp32 accumulate into main_grad).
+# MINGPT_LMHEAD_BLAS=0 puts the forward on gemm.hip; MINGPT_LMHEAD_DGRAD_BLAS=1 the data gradient
+# on the library.
 _LMHEAD_BLAS = os.environ.get("MINGPT_LMHEAD_BLAS", "1") == "1"
+_LMHEAD_DGRAD_BLAS = os.environ.get("MINGPT_LMHEAD_DGRAD_BLAS", "0") == "1"
 # Training cross-entropy in one pass over the logits (xent.hip xent_fused: loss and
 # dlogits = (softmax - onehot) / n_valid written in forward, grad_out applied in backward).
 # MINGPT_XENT_FUSED=0 keeps the two-pass fwd / bwd kernels.
@@ -248,7 +254,7 @@ class HeadLossFn(_EngineFn):
         del logits
         bw, mw = grad_target(w)
         G.gemm_tn_acc(dlogits, h, bw, n_valid=V)
-        if ctx.wpad is not None:
+        if ctx.wpad is not None and _LMHEAD_DGRAD_BLAS:
             dh = torch.mm(dlogits, ctx.wpad)  # zero rows past V meet the zero pad columns
         else:
             dh = G.gemm_dgrad(dlogits, w)  # W^T padded to the logits' row stride (zero columns)

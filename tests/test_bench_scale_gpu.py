@@ -46,7 +46,7 @@ def test_gpt2_width_fwd_bwd_matches_fp32(reference, monkeypatch, blas):
     cpu, x, y, ref = reference
     M = B * T
     assert fused._big(M, 768, 768) and fused._big(M, 50304, 768)  # every routing threshold is met
-    for flag in ("_DGRAD_BLAS", "_QKV_BLAS", "_LMHEAD_BLAS"):
+    for flag in ("_DGRAD_BLAS", "_QKV_BLAS", "_LMHEAD_BLAS", "_LMHEAD_DGRAD_BLAS"):
         monkeypatch.setattr(fused, flag, blas)
     gpu = copy.deepcopy(cpu).cuda().to(torch.bfloat16)
     logits, loss = gpu(x.cuda(), y.cuda())
