@@ -33,8 +33,20 @@ def _worker(rank, world, port, a, zero1, q):
         loss = eng.train_step([(x, x)])
     torch.cuda.synchronize()
     opt_bytes = (eng.opt.exp_avg.numel() + eng.opt.exp_avg_sq.numel()) * 4
+    peak_train = torch.cuda.max_memory_allocated()
+    # snapshot cost: what a checkpoint adds on the device on top of training's resident state
+    # (ZeRO-1 consolidate() gathers the moments into rank-0 HOST memory, one bucket at a time)
+    torch.cuda.reset_peak_memory_stats()
+    base = torch.cuda.memory_allocated()
+    if hasattr(eng.opt, "consolidate"):
+        eng.opt.consolidate()
+    if rank == 0:
+        sd = eng.opt.state_dict()
+        del sd
+    torch.cuda.synchronize()
     q.put({"rank": rank, "zero1": zero1, "loss": float(loss), "opt_state_gb": opt_bytes / 1e9,
-           "max_alloc_gb": torch.cuda.max_memory_allocated() / 1e9})
+           "max_alloc_gb": peak_train / 1e9,
+           "snapshot_extra_gb": (torch.cuda.max_memory_allocated() - base) / 1e9})
     D.destroy()
 
 
