@@ -286,13 +286,18 @@ class FusedAdamW:
     def rehome(self, new_store: FlatParamStore):
         """Move the moments to ``new_store``'s layout (same parameters, other order/padding)."""
         old = self.store
-        m = torch.zeros(new_store.total, dtype=torch.float32, device=new_store.device)
-        v = torch.zeros_like(m)
-        for name, o, n in zip(old.names, old.offsets, old.numels):
-            k = new_store.by_name[name]
-            no = new_store.offsets[k]
-            m[no:no + n].copy_(self.exp_avg[o:o + n])
-            v[no:no + n].copy_(self.exp_avg_sq[o:o + n])
+
+        def moved(buf):  # one new-layout buffer at a time: at most one extra moment buffer alive
+            out = torch.zeros(new_store.total, dtype=torch.float32, device=new_store.device)
+            for name, o, n in zip(old.names, old.offsets, old.numels):
+                no = new_store.offsets[new_store.by_name[name]]
+                out[no:no + n].copy_(buf[o:o + n])
+            return out
+
+        m = moved(self.exp_avg)
+        self.exp_avg = None
+        v = moved(self.exp_avg_sq)
+        self.exp_avg_sq = None
         sd_step = self.step_count
         self.__init__(new_store, lr=self.param_groups[0]["lr"], betas=self.betas, eps=self.eps,
                       weight_decay=self.weight_decay, decay_names=self.decay_names,

@@ -117,9 +117,17 @@ class StepEngine:
         fp32 masters and Adam moments (DDP's bucket rebuild after iteration 1)."""
         old_store, old_dp = self.store, self.dp
         old_dp.close()
+        old_dp.comm = None  # its bf16 reduce buffer; the new engine allocates its own
+        # transient memory: the old gradient buffer holds nothing needed after the optimizer step
+        # (the new store starts from zero grads), so it goes first; the moments are moved one
+        # buffer at a time (FusedAdamW.rehome)
+        old_store.grad = None
+        for p in old_store.params:
+            p.main_grad = None
         new = FlatParamStore(self.model, device=self.device,
                              bucket_numel=DataParallelEngine.bucket_numel(self.bucket_mb),
                              order=order, master_from=old_store)
+        old_store.master = old_store.flat = None  # copied into `new`; only its layout is read below
         self.opt.rehome(new)
         self.store = new
         self.dp = DataParallelEngine(new, bucket_mb=self.bucket_mb, reduce_dtype=self.reduce_dtype,
