@@ -4,18 +4,17 @@ Granularity is chosen for the MI355X, not for module boundaries: one Function pe
 block (LN1 -> QKV GEMM+bias -> flash attention -> proj GEMM with fused bias+dropout+residual ->
 LN2 -> FC GEMM with fused bias+GELU -> proj GEMM with fused bias+dropout+residual), one for the
 embedding and one for final-LN + LM head + cross-entropy.  Every norm, attention, loss and
-elementwise op and every GEMM of a transformer block (the fused-epilogue ones -- bias+GELU,
-bias+dropout+residual, GELU', the weight gradients with their fp32 accumulation -- and the plain
-ones: the qkv projection and the three data gradients) is a hand-written HIP kernel; so are the
-LM head's weight and data gradients.  One GEMM runs on the library (hipBLASLt through torch.mm):
-the LM head's forward ([M, 768] x [768, 50304], 6.6 GB of logits written at K = 768), where
-hipBLASLt is 1.7 % of the B=64 step faster than the W4 kernel (one-box A/B, PERF.md), as the
-project brief allows for plain library GEMMs.  ``MINGPT_LMHEAD_BLAS=0`` puts it on gemm.hip too
-(the all-HIP path, also tested and benchmarked); ``MINGPT_QKV_BLAS=1 MINGPT_DGRAD_BLAS=1
-MINGPT_LMHEAD_DGRAD_BLAS=1`` restores round 1's library routing of the plain block GEMMs, which
-measured equal in the step once the W4 main loop improved.  Weight gradients are accumulated in
-fp32 straight into ``param.main_grad`` (see ``grads.py``) so the data-parallel engine can
-all-reduce a bucket the moment its last gradient lands.
+elementwise op and every GEMM -- the fused-epilogue ones (bias+GELU, bias+dropout+residual,
+GELU', the weight gradients with their fp32 accumulation), the plain ones of a block (qkv
+projection, the three data gradients) and the LM head's forward, weight and data gradients -- is
+a hand-written HIP kernel: no library GEMM runs in the default step.  ``MINGPT_LMHEAD_BLAS=1``
+puts the LM head's forward on hipBLASLt (through torch.mm), which is 1.2 % of the B=64 step
+faster there (K = 768 with 6.6 GB of logits written; PERF.md), as the project brief allows for
+plain library GEMMs; ``MINGPT_QKV_BLAS=1 MINGPT_DGRAD_BLAS=1 MINGPT_LMHEAD_DGRAD_BLAS=1`` restores
+round 1's library routing of the other plain GEMMs (equal in the step once the W4 main loop
+improved).  Weight gradients are accumulated in fp32 straight into ``param.main_grad`` (see
+``grads.py``) so the data-parallel engine can all-reduce a bucket the moment its last gradient
+lands.
 
 Reference anchors: block structure ``/root/reference/mingpt/model.py:171-189`` (with D4/D5/D6
 fixed), embedding ``model.py:193-231``, head + loss ``model.py:309-320``.
@@ -185,13 +184,12 @@ class TransformerBlockFn(_EngineFn):
 
 # ------------------------------------------------------------------------------------ head + loss
 # The LM head's forward carries no epilogue (plain [M, 768] x [768, 50304], K = 768, 6.6 GB of
-# logits written): it goes to the library GEMM (hipBLASLt via torch.mm against a zero-padded
-# weight copy), 4.1 vs 5.0 ms per call on the W4 kernel (bench/gemm_blas_shapes.py) -- 1.7 % of the
-# step.  Its data gradient ([M, 50304] x [50304, 768], K = 50304) runs on gemm.hip (the 128x96-wave
-# W4 tile: 3.75 vs 3.81 ms), the weight gradient too (fp32 accumulate into main_grad).
-# MINGPT_LMHEAD_BLAS=0 puts the forward on gemm.hip; MINGPT_LMHEAD_DGRAD_BLAS=1 the data gradient
-# on the library.
-_LMHEAD_BLAS = os.environ.get("MINGPT_LMHEAD_BLAS", "1") == "1"
+# logits written): gemm.hip's W4 kernel by default (5.0 ms per call at B = 64), hipBLASLt via
+# torch.mm against a zero-padded weight copy with MINGPT_LMHEAD_BLAS=1 (4.1 ms, +1.2 % step).  Its
+# data gradient ([M, 50304] x [50304, 768], K = 50304) runs on gemm.hip (the 128x96-wave W4 tile:
+# 3.75 vs 3.81 ms), the weight gradient too (fp32 accumulate into main_grad).
+# MINGPT_LMHEAD_DGRAD_BLAS=1 (with MINGPT_LMHEAD_BLAS=1) puts the data gradient on the library.
+_LMHEAD_BLAS = os.environ.get("MINGPT_LMHEAD_BLAS", "0") == "1"
 _LMHEAD_DGRAD_BLAS = os.environ.get("MINGPT_LMHEAD_DGRAD_BLAS", "0") == "1"
 # Training cross-entropy in one pass over the logits (xent.hip xent_fused: loss and
 # dlogits = (softmax - onehot) / n_valid written in forward, grad_out applied in backward).
