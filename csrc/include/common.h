@@ -68,6 +68,11 @@ MG_DEVICE uint64_t eff_seed(uint64_t s, const uint64_t* ofs) {
 // instead of being kept live (keeps packed bf16 packed across a reduction; see layernorm.hip).
 MG_DEVICE void reg_fence(uint4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
 MG_DEVICE void st16(void* p, const uint4& v) { *reinterpret_cast<uint4*>(p) = v; }
+// non-temporal 16-byte store (a large output consumed by a later kernel: keep L2 / MALL for inputs)
+MG_DEVICE void st16_nt(void* p, const uint4& v) {
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(p));
+}
 
 // ---------------------------------------------------------------- wave / block reductions
 MG_DEVICE float wave_sum(float v) {

@@ -715,11 +715,12 @@ __global__ __launch_bounds__(256) void attn_dq_finalize_kernel(const float* __re
   for (int k = 0; k < np; k += 4) {  // four partials' loads in flight before the adds
     float4 y[4][2];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 4; ++u) {  // partials are read once: non-temporal
       const bool ok = k + u < np;
       const float* s = src + (long)(ok ? k + u : k) * part;
-      y[u][0] = ok ? *reinterpret_cast<const float4*>(s) : make_float4(0.f, 0.f, 0.f, 0.f);
-      y[u][1] = ok ? *reinterpret_cast<const float4*>(s + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const uint4 a0 = ok ? ld16_nt(s) : make_uint4(0, 0, 0, 0), a1 = ok ? ld16_nt(s + 4) : make_uint4(0, 0, 0, 0);
+      y[u][0] = make_float4(__uint_as_float(a0.x), __uint_as_float(a0.y), __uint_as_float(a0.z), __uint_as_float(a0.w));
+      y[u][1] = make_float4(__uint_as_float(a1.x), __uint_as_float(a1.y), __uint_as_float(a1.z), __uint_as_float(a1.w));
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -728,7 +729,7 @@ __global__ __launch_bounds__(256) void attn_dq_finalize_kernel(const float* __re
     }
   }
   const float f[8] = {x0.x * sc, x0.y * sc, x0.z * sc, x0.w * sc, x1.x * sc, x1.y * sc, x1.z * sc, x1.w * sc};
-  st16(dqkv + (long)r * 3L * D + c, pack8(f));
+  st16_nt(dqkv + (long)r * 3L * D + c, pack8(f));
 }
 
 template <int NKS, int KW>

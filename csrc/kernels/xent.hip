@@ -145,7 +145,7 @@ __global__ __launch_bounds__(1024) void xent_fused_kernel(const bf16_t* __restri
   for (int k = 0; k < NV; ++k) {  // every load issued before any math: NV x 16 B in flight/lane
     const int c = (threadIdx.x + k * 1024) * 8;
     if (c + 8 <= V) {
-      u[k] = ld16(lr + c);
+      u[k] = ld16_nt(lr + c);  // read once
     } else if (c < V) {
       float f[8];
 #pragma unroll
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(1024) void xent_fused_kernel(const bf16_t* __restri
       unpack8(u[k], v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = g * (exp2f(fmaf(v[j], L2E, -lb)) - ((c + j) == t ? 1.f : 0.f));
-      st16(dr + c, pack8(v));
+      st16_nt(dr + c, pack8(v));  // 6.6 GB at GPT-2 B = 64: bypass L2 / MALL
     }
   }
   if (threadIdx.x == 0) loss_row[row] = (t < 0) ? 0.f : lse - bf2f(lr[t]);
