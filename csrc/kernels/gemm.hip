@@ -1152,7 +1152,10 @@ int pick_config(int M, int N, int K, int layout) {
     const long r256 = (t256 + 255) / 256 * 256, r192 = (tm * cdiv(N, 192) + 255) / 256 * 192;
     return r192 * 108 < r256 * 100 ? 6 : 5;
   }
-  if (layout == 1) return (K >= 1536 || t256 >= 1024) ? 4 : 1;
+  // dgrad (NN, the weight read in place through the transposing LDS reads): W4 at every block
+  // shape (bench/dgrad_nn_vs_nt.py, M = 65536: proj 84 / PP 97 us, fc 251 / 290, qkv 182 / 210,
+  // fc2 + GELU' 344 / 362), and faster than NT against a transposed weight copy
+  if (layout == 1) return t256 >= 256 ? 5 : 1;
   return (long)M * N >= (1L << 20) ? 5 : 1;  // wgrad: W4 since the asm tr reads (bench_wgrad.py)
 }
 

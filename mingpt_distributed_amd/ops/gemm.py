@@ -9,12 +9,13 @@ epilogue fused where the data is produced.
                    epilogue: ``none`` | ``gelu_bwd`` (multiply by aux = GELU'(z) from the forward)
 * ``gemm_tn_acc``  C[N,K] += A[M,N]^T @ B[M,K] (weight gradient, fp32 accumulate into main_grad)
 
-All three run on the hand-written MFMA kernels in ``csrc/kernels/gemm.hip`` (``_C.gemm``).  The
-training step (``ops/fused.py``) routes the large epilogue-free GEMMs to hipBLASLt instead (see
-its module docstring; ``MINGPT_*_BLAS=0`` keeps them here).
+All three run on the hand-written MFMA kernels in ``csrc/kernels/gemm.hip`` (``_C.gemm``); the
+training step (``ops/fused.py``) uses nothing else by default (``MINGPT_*_BLAS=1`` switches route
+some plain GEMMs to hipBLASLt, see its module docstring).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -25,6 +26,8 @@ EPI_NONE, EPI_BIAS, EPI_GELU, EPI_RESID, EPI_GELU_BWD = 0, 1, 2, 3, 4
 
 
 _MAX_BYTES = 0xFFFFFF00  # the kernels address each operand through a 32-bit buffer descriptor
+# data gradients NN from the stored weight (MINGPT_DGRAD_NN=0: NT against a transposed copy)
+_DGRAD_NN = os.environ.get("MINGPT_DGRAD_NN", "1") == "1"
 
 
 def _row_chunks(M: int, *row_bytes: int):
@@ -81,8 +84,13 @@ def transpose(w: torch.Tensor, ld: Optional[int] = None) -> torch.Tensor:
 def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, *, epi: str = "none",
                aux: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None,
                dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """dX = dY @ W (W [N_out, N_in] as stored by nn.Linear), as NT against W^T.  With
-    ``epi="gelu_bwd"`` and ``dbias``, the bias gradient of the result is accumulated in the epilogue."""
+    """dX = dY @ W (W [N_out, N_in] as stored by nn.Linear).  Block shapes run NN straight from the
+    stored weight (the W4 kernel's transposing LDS reads; no per-step transposed copy:
+    bench/dgrad_nn_vs_nt.py); a long reduction (the LM head's K = vocab) or ``dbias`` runs NT
+    against W^T, where the 128x96-wave W4 tile applies.  With ``epi="gelu_bwd"`` and ``dbias``, the
+    bias gradient of the result is accumulated in the epilogue."""
+    if _DGRAD_NN and wt is None and dbias is None and dy.shape[1] < 8192 and w.shape[0] == dy.shape[1]:
+        return gemm_nn(dy, w, epi=epi, aux=aux)
     if wt is None:
         wt = transpose(w, dy.shape[1])
     return gemm_nt(dy, wt, epi=epi, aux=aux, dbias=dbias)
