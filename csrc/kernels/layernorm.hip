@@ -3,9 +3,9 @@
 // Replaces the reference's three ATen LayerNorms per block (ln_1, ln_2, ln_ff:
 // /root/reference/mingpt/model.py:176,178,248).  Layout: x is [M, D] bf16 row-major.
 //
-// Forward: one wave per row, 4 rows per 256-thread block; each lane holds NV chunks of 8
-// contiguous bf16 (16-B loads), so the row is read from HBM exactly once and the two-pass
-// (mean, then centred variance) statistics come from registers.  mean/rstd are saved in fp32.
+// Forward: two rows per wave, 8 rows per 256-thread block; each lane holds NV chunks of 8
+// contiguous bf16 (16-B loads) of both rows, so a row is read from HBM exactly once and the
+// two-pass (mean, then centred variance) statistics come from registers.  mean/rstd in fp32.
 //
 // Backward: same row mapping.  dx is produced per row (optionally + the residual-branch gradient);
 // dgamma/dbeta are accumulated per wave in registers over a grid-stride loop, folded across the
@@ -25,53 +25,63 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
                                                      bf16_t* __restrict__ y, float* __restrict__ mean,
                                                      float* __restrict__ rstd, int M, int D,
                                                      float eps) {
+  // two rows per wave (rows r and r + 4 of the block's 8): both rows' loads are issued before
+  // either is reduced, so a wave keeps twice the bytes in flight
   const int lane = threadIdx.x & 63;
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
-  const bf16_t* xr = x + row * D;
-  float v[NV][8];
-  float s = 0.f;
+  const long r0 = (long)blockIdx.x * 8 + (threadIdx.x >> 6);
+  if (r0 >= M) return;
+  const long rows[2] = {r0, r0 + 4 < M ? r0 + 4 : r0};
+  const bool two = r0 + 4 < M;
+  uint4 raw[2][NV];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = (i * 64 + lane) * 8;
-    if (c < D) {
-      unpack8(ld16(xr + c), v[i]);
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      raw[u][i] = c < D ? ld16(x + rows[u] * D + c) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (u == 1 && !two) break;
+    const long row = rows[u];
+    float v[NV][8];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      unpack8(raw[u][i], v[i]);  // zero past D
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += v[i][j];
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
     }
-  }
-  const float mu = wave_sum(s) / D;
-  float ss = 0.f;
+    const float mu = wave_sum(s) / D;
+    float ss = 0.f;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = (i * 64 + lane) * 8;
-    if (c < D) {
+    for (int i = 0; i < NV; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      if (c < D) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float d = v[i][j] - mu;
-        ss += d * d;
+        for (int j = 0; j < 8; ++j) {
+          const float d = v[i][j] - mu;
+          ss += d * d;
+        }
       }
     }
-  }
-  const float rs = rsqrtf(wave_sum(ss) / D + eps);
-  if (lane == 0) {
-    mean[row] = mu;
-    rstd[row] = rs;
-  }
-  bf16_t* yr = y + row * D;
+    const float rs = rsqrtf(wave_sum(ss) / D + eps);
+    if (lane == 0) {
+      mean[row] = mu;
+      rstd[row] = rs;
+    }
+    bf16_t* yr = y + row * D;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = (i * 64 + lane) * 8;
-    if (c < D) {
-      float wf[8], bf[8], o[8];
-      unpack8(ld16(w + c), wf);
-      unpack8(ld16(b + c), bf);
+    for (int i = 0; i < NV; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      if (c < D) {
+        float wf[8], bf[8], o[8];
+        unpack8(ld16(w + c), wf);
+        unpack8(ld16(b + c), bf);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mu) * rs * wf[j] + bf[j];
-      st16(yr + c, pack8(o));
+        for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mu) * rs * wf[j] + bf[j];
+        st16(yr + c, pack8(o));
+      }
     }
   }
 }
@@ -260,7 +270,7 @@ int ln_bwd_grid(int M, int D) {
 
 void layernorm_fwd(const bf16_t* x, const bf16_t* w, const bf16_t* b, bf16_t* y, float* mean,
                    float* rstd, int M, int D, float eps, hipStream_t stream) {
-  const int grid = cdiv(M, 4);
+  const int grid = cdiv(M, 8);  // 8 rows per block: two per wave
   const size_t smem = 0;
   MG_LN_DISPATCH(ln_fwd_kernel, x, w, b, y, mean, rstd, M, D, eps);
 }
