@@ -72,9 +72,13 @@ at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Te
 }
 
 // ------------------------------------------------------------------------------- embedding
-// pos_dev (int32 [1], optional; decode with T == 1): the position row of wpe is read on the device
+// pos_dev (int32 [1], optional; decode with T == 1): the position row of wpe is read on the device.
+// am_part (int64 [B, G], optional, with pos_dev): greedy decode -- the token of row b is the argmax
+// of the previous step's LM-head keys am_part[b] (gemv with am_part), written to tok[b] (idx may
+// be that same buffer) and to seq[b, pos] when given.
 at::Tensor embedding_fwd(const at::Tensor& idx, const at::Tensor& wte, const at::Tensor& wpe,
-                         double p, int64_t seed, const c10::optional<at::Tensor>& pos_dev) {
+                         double p, int64_t seed, const c10::optional<at::Tensor>& pos_dev,
+                         const c10::optional<at::Tensor>& am_part, const c10::optional<at::Tensor>& seq) {
   CHECK_I64(idx); CHECK_BF16(wte); CHECK_BF16(wpe); CHECK_CONTIG(idx);
   CHECK_CONTIG(wte); CHECK_CONTIG(wpe);
   TORCH_CHECK(idx.dim() == 2, "idx must be [B, T]");
@@ -86,10 +90,27 @@ at::Tensor embedding_fwd(const at::Tensor& idx, const at::Tensor& wte, const at:
                 "embedding_fwd: pos_dev (int32 cuda) is for one-token decode steps");
     pd = pos_dev->data_ptr<int>();
   }
+  const unsigned long long* ap = nullptr;
+  int groups = 0;
+  int64_t* seqp = nullptr;
+  long seq_ld = 0;
+  if (am_part.has_value()) {
+    TORCH_CHECK(pd && am_part->scalar_type() == at::kLong && am_part->is_contiguous() && am_part->dim() == 2 &&
+                am_part->size(0) == B, "embedding_fwd: am_part int64 [B, G] with pos_dev");
+    ap = reinterpret_cast<const unsigned long long*>(am_part->data_ptr<int64_t>());
+    groups = (int)am_part->size(1);
+    if (seq.has_value()) {
+      TORCH_CHECK(seq->scalar_type() == at::kLong && seq->is_contiguous() && seq->dim() == 2 && seq->size(0) == B,
+                  "embedding_fwd: seq int64 [B, L]");
+      seqp = seq->data_ptr<int64_t>();
+      seq_ld = seq->size(1);
+    }
+  }
   DevGuard g(idx.device());
   auto out = at::empty({B, T, D}, wte.options());
   mg::embedding_fwd(idx.data_ptr<int64_t>(), bp(wte), bp(wpe), bp(out), (int)(B * T), (int)T,
-                    (int)D, (int)wte.size(0), (float)p, (uint64_t)seed, cur_stream(), pd);
+                    (int)D, (int)wte.size(0), (float)p, (uint64_t)seed, cur_stream(), pd, ap, groups,
+                    ap ? idx.data_ptr<int64_t>() : nullptr, seqp, seq_ld);
   return out;
 }
 
@@ -429,8 +450,8 @@ at::Tensor attention_bwd(const at::Tensor& qkv, const at::Tensor& out, const at:
 // y[B, ldy] (ldy >= N) = epi(x[B, K] @ W[N, K]^T): the decode-time projection (gemv.hip)
 at::Tensor gemv(const at::Tensor& x, const at::Tensor& W, int64_t epi, const c10::optional<at::Tensor>& bias,
                 const c10::optional<at::Tensor>& resid, int64_t ldy, const c10::optional<at::Tensor>& lnw,
-                const c10::optional<at::Tensor>& lnb, double eps, const c10::optional<at::Tensor>& am_tok,
-                const c10::optional<at::Tensor>& am_pos, const c10::optional<at::Tensor>& am_seq) {
+                const c10::optional<at::Tensor>& lnb, double eps, const c10::optional<at::Tensor>& am_part,
+                const c10::optional<at::Tensor>& am_pos) {
   CHECK_BF16(x); CHECK_BF16(W); CHECK_CONTIG(x); CHECK_CONTIG(W);
   const int64_t K = W.size(1), N = W.size(0), B = x.numel() / K;
   TORCH_CHECK(x.size(-1) == K && mg::gemv_supported((int)B, (int)K), "gemv: B <= 8, K % 8 == 0, K <= 4096");
@@ -449,49 +470,22 @@ at::Tensor gemv(const at::Tensor& x, const at::Tensor& W, int64_t epi, const c10
   }
   DevGuard g(x.device());
   mg::GemvArgmax am{};
-  if (am_tok.has_value()) {
-    // greedy decode: fused argmax (the LM head, N > 8192 rows) -> am_tok [B] int64, am_seq[b, pos+1],
-    // *am_pos += 1.  Workspace: one 8-byte partial per (row, workgroup) and an arrival counter,
-    // allocated outside graph capture (the first, eager call) and left zeroed by the kernel.
+  if (am_part.has_value()) {
+    // greedy decode: the LM-head GEMV (N > 8192 rows) also leaves one argmax key per (row,
+    // workgroup) in am_part [B, gemv_grid(N)] (int64 storage of the unsigned keys) and advances
+    // *am_pos; the next step's embedding_fwd(am_part=...) reduces the keys into the token
     TORCH_CHECK(N > 8192 && epi == 0, "gemv argmax: LM-head shape (N > 8192, no epilogue)");
-    TORCH_CHECK(am_tok->scalar_type() == at::kLong && am_tok->numel() == B && am_tok->is_cuda() &&
-                am_pos.has_value() && am_pos->scalar_type() == at::kInt && am_pos->is_cuda(),
-                "gemv argmax: am_tok int64 [B], am_pos int32 [1]");
-    static unsigned long long* part = nullptr;
-    static unsigned* cnt = nullptr;
-    static size_t part_n = 0, cnt_n = 0;
-    const size_t need = mg::gemv_argmax_part_words((int)B, (int)N), needc = mg::gemv_argmax_counters((int)N);
-    if (need > part_n || needc > cnt_n) {
-      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-      hipStreamIsCapturing(cur_stream(), &cs);
-      TORCH_CHECK(cs == hipStreamCaptureStatusNone, "gemv argmax: first call must not be inside a graph capture");
-      if (need > part_n) {
-        if (part) hipFree(part);
-        hipMalloc(&part, need * sizeof(unsigned long long));
-        part_n = need;
-      }
-      if (needc > cnt_n) {
-        if (cnt) hipFree(cnt);
-        hipMalloc(&cnt, needc * sizeof(unsigned));
-        hipMemset(cnt, 0, needc * sizeof(unsigned));
-        cnt_n = needc;
-      }
-      hipDeviceSynchronize();
-    }
-    am.part = part; am.cnt = cnt;
-    am.tok = am_tok->data_ptr<int64_t>();
+    TORCH_CHECK(am_part->scalar_type() == at::kLong && am_part->is_cuda() && am_part->is_contiguous() &&
+                am_part->numel() == B * mg::gemv_grid((int)N), "gemv argmax: am_part int64 [B, gemv_argmax_groups(N)]");
+    TORCH_CHECK(am_pos.has_value() && am_pos->scalar_type() == at::kInt && am_pos->is_cuda(),
+                "gemv argmax: am_pos int32 [1]");
+    am.part = reinterpret_cast<unsigned long long*>(am_part->data_ptr<int64_t>());
     am.pos = am_pos->data_ptr<int>();
-    if (am_seq.has_value()) {
-      TORCH_CHECK(am_seq->scalar_type() == at::kLong && am_seq->dim() == 2 && am_seq->size(0) == B &&
-                  am_seq->is_contiguous(), "gemv argmax: am_seq int64 [B, L]");
-      am.seq = am_seq->data_ptr<int64_t>();
-      am.seq_ld = am_seq->size(1);
-    }
   }
   auto y = at::empty({B, ldy}, x.options());
   mg::gemv(bp(x), bp(W), bp(y), (int)B, (int)N, (int)K, ldy, bias.has_value() ? bp(*bias) : nullptr,
            epi == 3 ? bp(*resid) : nullptr, (int)epi, cur_stream(), bp_opt(lnw), bp_opt(lnb), (float)eps,
-           am_tok.has_value() ? &am : nullptr);
+           am_part.has_value() ? &am : nullptr);
   return y;
 }
 
@@ -523,7 +517,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("embedding_fwd", &embedding_fwd, py::arg("idx"), py::arg("wte"), py::arg("wpe"), py::arg("p"),
-        py::arg("seed"), py::arg("pos_dev") = py::none());
+        py::arg("seed"), py::arg("pos_dev") = py::none(), py::arg("am_part") = py::none(),
+        py::arg("seq") = py::none());
   // debug builds: OR of the device error words (1/2 = token id out of range in embedding fwd/bwd,
   // 4 = cross-entropy target >= V), cleared on read; always 0 in release builds
   m.def("debug_error_bits", []() -> int64_t { return (int64_t)mg::debug_error_bits(); });
@@ -561,8 +556,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attention_bwd", &attention_bwd);
   m.def("gemv", &gemv, py::arg("x"), py::arg("W"), py::arg("epi"), py::arg("bias") = py::none(),
         py::arg("resid") = py::none(), py::arg("ldy") = 0, py::arg("lnw") = py::none(),
-        py::arg("lnb") = py::none(), py::arg("eps") = 1e-5, py::arg("am_tok") = py::none(),
-        py::arg("am_pos") = py::none(), py::arg("am_seq") = py::none());
+        py::arg("lnb") = py::none(), py::arg("eps") = 1e-5, py::arg("am_part") = py::none(),
+        py::arg("am_pos") = py::none());
+  m.def("gemv_argmax_groups", [](int64_t N) { return (int64_t)mg::gemv_grid((int)N); });
   m.def("gemv_supported", &mg::gemv_supported);
   m.def("attention_decode", &attention_decode, py::arg("qkv_new"), py::arg("cache"), py::arg("H"),
         py::arg("pos"), py::arg("pos_dev") = py::none());

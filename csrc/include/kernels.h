@@ -20,7 +20,12 @@ size_t layernorm_bwd_workspace(int M, int D);
 // embedding.hip
 void embedding_fwd(const int64_t* idx, const bf16_t* wte, const bf16_t* wpe, bf16_t* out, int M,
                    int T, int D, int V, float p, uint64_t seed, hipStream_t stream,
-                   const int* pos_dev = nullptr);  // pos_dev: decode, position read on the device
+                   const int* pos_dev = nullptr,  // pos_dev: decode, position read on the device
+                   const unsigned long long* am_part = nullptr,  // greedy decode: the token of row m
+                   int am_groups = 0,             //   = argmax over the LM-head GEMV's keys
+                   int64_t* tok = nullptr,        //   am_part[m][0 .. am_groups), written to tok[m]
+                   int64_t* seq = nullptr,        //   and seq[m * seq_ld + *pos_dev]
+                   long seq_ld = 0);
 unsigned int debug_error_bits();  // MG_DEBUG builds: device range-check bits, cleared on read
 void embedding_bwd(const int64_t* idx, const bf16_t* dout, float* dwte, float* dwpe, int M, int T,
                    int D, int V, float p, uint64_t seed, hipStream_t stream);
@@ -54,19 +59,15 @@ void f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t stream);
 
 // gemv.hip (decode-time skinny GEMM, B <= 8 rows; epi 0 none, 1 bias, 2 bias+GELU, 3 bias+residual)
 bool gemv_supported(int B, int K);
-// greedy-decode epilogue of the LM-head GEMV: argmax of each row's (bf16) logits, first index on
-// ties; the last workgroup writes tok[b], seq[b * seq_ld + pos + 1] and advances *pos
+// greedy-decode epilogue of the LM-head GEMV: each workgroup's best (ordered bf16 logit << 32 |
+// ~index) key per row into part[b][workgroup]; workgroup 0 advances *pos.  The argmax over the
+// workgroups (first index on ties) is taken by the next step's embedding kernel (embedding_fwd
+// with am_part) or on the host after the last step.
 struct GemvArgmax {
-  unsigned long long* part;  // [B][grid] per-workgroup best (ordered-key << 32 | ~index)
-  unsigned* cnt;             // arrival counters (left zero)
-  int64_t* tok;              // [B] next token (the next decode step's input)
-  int64_t* seq;              // [B, seq_ld] token buffer or nullptr
-  long seq_ld;
-  int* pos;                  // device position of the step (read, then +1)
+  unsigned long long* part;  // [B][gemv_grid(N)]
+  int* pos;                  // device position of the step (+1)
 };
 int gemv_grid(int N);
-size_t gemv_argmax_part_words(int B, int N);
-size_t gemv_argmax_counters(int N);
 void gemv(const bf16_t* x, const bf16_t* W, bf16_t* y, int B, int N, int K, long ldy, const bf16_t* bias,
           const bf16_t* resid, int epi, hipStream_t stream, const bf16_t* lnw = nullptr,
           const bf16_t* lnb = nullptr, float eps = 1e-5f, const GemvArgmax* am = nullptr);

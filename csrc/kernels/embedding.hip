@@ -22,12 +22,37 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict_
                                                       unsigned int* __restrict__ err,
                                                       uint64_t seed, uint32_t thr, float scale,
                                                       int use_dropout, const uint64_t* sofs,
-                                                      const int* __restrict__ pos_dev) {
+                                                      const int* __restrict__ pos_dev,
+                                                      const unsigned long long* __restrict__ am_part,
+                                                      int am_groups, int64_t* __restrict__ tok_out,
+                                                      int64_t* __restrict__ seq, long seq_ld) {
   const int lane = threadIdx.x & 63;
   const long m = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= M) return;
   seed = eff_seed(seed, sofs);
-  long tok = idx[m];
+  long tok;
+  if (am_part) {
+    // greedy decode: this row's token is the argmax the previous step's LM-head GEMV left as one
+    // key per workgroup (gemv.hip): a wave max over the keys, first index on ties
+    unsigned long long best = 0;
+    for (int i = lane; i < am_groups; i += 64) {
+      const unsigned long long k = am_part[m * am_groups + i];
+      best = k > best ? k : best;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned lo = __shfl_xor((unsigned)best, o, 64), hi = __shfl_xor((unsigned)(best >> 32), o, 64);
+      const unsigned long long k = ((unsigned long long)hi << 32) | lo;
+      best = k > best ? k : best;
+    }
+    tok = (long)(0xffffffffu - (uint32_t)best);
+    if (lane == 0) {
+      if (tok_out) tok_out[m] = tok;
+      if (seq) seq[m * seq_ld + *pos_dev] = tok;
+    }
+  } else {
+    tok = idx[m];
+  }
   MG_CHECK_INDEX(tok, tok >= 0 && tok < V, 0, err, 1u)
   const int t = pos_dev ? *pos_dev : (int)(m % T);  // decode step: one token at a device position
   for (int c = lane * 8; c < D; c += 512) {
@@ -107,11 +132,14 @@ __global__ __launch_bounds__(64) void emb_bwd_wpe_kernel(const bf16_t* __restric
 namespace mg {
 
 void embedding_fwd(const int64_t* idx, const bf16_t* wte, const bf16_t* wpe, bf16_t* out, int M,
-                   int T, int D, int V, float p, uint64_t seed, hipStream_t stream, const int* pos_dev) {
+                   int T, int D, int V, float p, uint64_t seed, hipStream_t stream, const int* pos_dev,
+                   const unsigned long long* am_part, int am_groups, int64_t* tok, int64_t* seq,
+                   long seq_ld) {
   const uint32_t thr = dropout_threshold8(p);  // the 8-bit residual-stream mask (common.h)
   emb_fwd_kernel<<<cdiv(M, 4), 256, 0, stream>>>(idx, wte, wpe, out, M, T, D, V, debug_err_word(), seed, thr,
                                                  dropout_scale8(thr), p > 0.f,
-                                                 graph_seed_ofs(), pos_dev);
+                                                 graph_seed_ofs(), pos_dev, am_part, am_groups, tok, seq,
+                                                 seq_ld);
 }
 
 void embedding_bwd(const int64_t* idx, const bf16_t* dout, float* dwte, float* dwpe, int M, int T,

@@ -17,9 +17,9 @@
 //   * weights are read non-temporally (streamed once per token; MI355X_MICROARCH launches-baseline:
 //     nt weight loads ~11 % faster per decode layer);
 //   * greedy decode (LM head): the argmax of the logits is fused -- each workgroup publishes its
-//     best (value, index) key with agent-scope stores, the last one to arrive reduces them and
-//     writes the next token and position on the device, so a captured decode step can be replayed
-//     back to back with no host round trip per token.
+//     best (value, index) key and the next decode step's embedding kernel reduces them into the
+//     token (and advances the device position), so a captured decode step can be replayed back
+//     to back with no host round trip per token.
 #include "common.h"
 #include "kernels.h"
 
@@ -47,82 +47,26 @@ MG_DEVICE unsigned long long wave_umax64(unsigned long long v) {
   return v;
 }
 
-// Fused greedy argmax over the 16 rows of this workgroup, then across workgroups in two levels
-// (groups of 64 workgroups, then the groups): thousands of arrivals on ONE counter serialise at
-// ~88 per us (MI355X_MICROARCH 'dequeue'), one counter per group keeps each word at <= 64.
-// Hand-off as in attn_decode_kernel: agent-scope (sc1) stores of the partial, every wave drains
-// them (vmcnt(0)) before the barrier and the counter increment, agent-scope loads by the last.
-constexpr int kAmGroup = 64;
-MG_DEVICE int am_groups(int G) { return (G + kAmGroup - 1) / kAmGroup; }
-
-// max key of n (<= 64 per pass) agent-scope partials per row b; wave w takes rows w, w + 4
-template <int B>
-MG_DEVICE void am_reduce(const unsigned long long* src, long ld, int n, unsigned long long (&out)[B],
-                         unsigned long long* sh) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int b = wid; b < B; b += 4) {
-    unsigned long long best = 0;
-    for (int i = lane; i < n; i += 64)
-      best = umax64(best, __hip_atomic_load(src + (long)b * ld + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    best = wave_umax64(best);
-    if (lane == 0) sh[b] = best;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int b = 0; b < B; ++b) out[b] = sh[b];
-}
-
+// Fused greedy argmax, first half: every workgroup publishes its best (value, index) key per row
+// to part[b][workgroup] with plain stores, and workgroup 0 advances the device position.  The
+// cross-workgroup reduction is the NEXT kernel's (the decode step's embedding kernel, at a launch
+// boundary: no atomics, no hand-off).  A last-arrival reduction inside this kernel cost ~5 us per
+// token (store drain + returning atomics on counters; MI355X_MICROARCH 'dequeue').
 template <int B>
 MG_DEVICE void gemv_argmax(const GemvArgmax& am, const unsigned long long (&key)[B], bool mine, int row) {
   __shared__ unsigned long long kk[B][16];
-  __shared__ unsigned long long sh[B];
-  __shared__ int last;
   if (mine) {  // this lane's best over the rows it produced (0: none)
 #pragma unroll
     for (int b = 0; b < B; ++b) kk[b][row] = key[b];
   }
   __syncthreads();
-  const int G = gridDim.x, NG = am_groups(G);
-  const int grp = blockIdx.x / kAmGroup, gsize = min(kAmGroup, G - grp * kAmGroup);
-  unsigned long long* p1 = am.part;           // [B][G]
-  unsigned long long* p2 = am.part + (long)B * G;  // [B][NG]
   if (threadIdx.x < B) {
     unsigned long long best = 0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) best = umax64(best, kk[threadIdx.x][r]);
-    __hip_atomic_store(p1 + (long)threadIdx.x * G + blockIdx.x, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    am.part[(long)threadIdx.x * gridDim.x + blockIdx.x] = best;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    last = __hip_atomic_fetch_add(am.cnt + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(gsize - 1);
-  __syncthreads();
-  if (!last) return;
-  // last of its group: the group's best -> level 2
-  unsigned long long best[B];
-  am_reduce<B>(p1 + (long)grp * kAmGroup, G, gsize, best, sh);
-  if (threadIdx.x < B)
-    __hip_atomic_store(p2 + (long)threadIdx.x * NG + grp, best[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(am.cnt + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = __hip_atomic_fetch_add(am.cnt + NG, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(NG - 1);
-  }
-  __syncthreads();
-  if (!last) return;
-  am_reduce<B>(p2, NG, NG, best, sh);
-  if (threadIdx.x == 0) {
-    const int pos = *am.pos;
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-      const int64_t t = (int64_t)(0xffffffffu - (uint32_t)best[b]);
-      am.tok[b] = t;
-      if (am.seq) am.seq[(long)b * am.seq_ld + pos + 1] = t;
-    }
-    *am.pos = pos + 1;
-    __hip_atomic_store(am.cnt + NG, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *am.pos += 1;  // nothing else in this kernel reads it
 }
 
 template <int B, int LPR>
@@ -362,12 +306,7 @@ int gemv_wide_cap() {
   return cap;
 }
 int gemv_grid(int N) { return N > 8192 ? min(cdiv(N, 16), gemv_wide_cap()) : cdiv(N, 4); }
-// argmax workspace: 8-byte partials per (row, workgroup) and per (row, group), counters per group + 1
-size_t gemv_argmax_part_words(int B, int N) {
-  const int G = gemv_grid(N);
-  return (size_t)B * (G + (G + kAmGroup - 1) / kAmGroup);
-}
-size_t gemv_argmax_counters(int N) { return (gemv_grid(N) + kAmGroup - 1) / kAmGroup + 1; }
+// argmax partials: one 8-byte key per (row, workgroup)
 
 void gemv(const bf16_t* x, const bf16_t* W, bf16_t* y, int B, int N, int K, long ldy, const bf16_t* bias,
           const bf16_t* resid, int epi, hipStream_t stream, const bf16_t* lnw, const bf16_t* lnb,
@@ -377,7 +316,7 @@ void gemv(const bf16_t* x, const bf16_t* W, bf16_t* y, int B, int N, int K, long
   // already launches thousands of workgroups and re-stages x in each)
   const bool wide = N > 8192;
   const int grid = gemv_grid(N);
-  const GemvArgmax amv = am ? *am : GemvArgmax{nullptr, nullptr, nullptr, nullptr, 0, nullptr};
+  const GemvArgmax amv = am ? *am : GemvArgmax{nullptr, nullptr};
 #define MG_GEMV_CASE(b)                                                                                        \
   case b:                                                                                                      \
     if (wide)                                                                                                  \

@@ -137,24 +137,33 @@ class _GpuCache:
 
     def _run(self, idx, pos0, pos_dev=None, greedy=None):
         """Prefill (pos0 == 0) or one decode step at position pos0 (or at ``pos_dev[0]``, an int32
-        device scalar, when captured in a hipGraph).  ``greedy`` = (tok [B] int64, pos_dev,
-        seq [B, Tmax + 1] int64): the LM-head kernel also takes the argmax, writes it to tok and
-        seq[:, pos + 1] and advances pos_dev -- the step then needs nothing from the host."""
+        device scalar, when captured in a hipGraph).  ``greedy`` = (tok [B, 1] int64, pos_dev,
+        seq [B, Tmax + 1] int64, part [B, G] int64 or None): the step needs nothing from the host.
+        With ``part`` (LM head on the skinny GEMM, V > 8192) the LM-head kernel leaves one argmax
+        key per (row, workgroup) in part and advances pos_dev, and the NEXT step's embedding
+        kernel reduces the keys into its input token (also written to tok and seq[:, pos]) --
+        no cross-workgroup hand-off inside a kernel.  Without it the argmax runs in torch and
+        writes tok and seq[:, pos + 1] itself."""
         C, G, bf = self.C, self.G, self.bf
         m = self.model
         tr, cfg = m.transformer, m.config
         B, T = idx.shape
         D, H, eps = cfg.n_embed, cfg.n_head, cfg.layer_norm_eps
         wpe = bf(tr.wpe.weight)
-        if pos0 == 0:
+        # decode rows (B <= 8) go through the skinny GEMM (gemv.hip): at M = B the MFMA GEMM has
+        # one row tile and walks K latency-bound; prefill uses the MFMA GEMM
+        skinny = pos0 > 0 and C.gemv_supported(B * T, 4 * D)
+        V = cfg.vocab_size
+        part = greedy[3] if greedy is not None else None
+        if part is not None:  # fused greedy: the token is the argmax of the previous LM head
+            x = C.embedding_fwd(idx, bf(tr.wte.weight), wpe, 0.0, 0, pos_dev, part,
+                                greedy[2]).view(B * T, D)
+        elif pos0 == 0:
             x = C.embedding_fwd(idx.contiguous(), bf(tr.wte.weight), wpe, 0.0, 0).view(B * T, D)
         elif pos_dev is not None:  # the position row is picked on the device (one kernel)
             x = C.embedding_fwd(idx.contiguous(), bf(tr.wte.weight), wpe, 0.0, 0, pos_dev).view(B * T, D)
         else:  # single token at position pos0
             x = C.embedding_fwd(idx.contiguous(), bf(tr.wte.weight), wpe[pos0:pos0 + 1], 0.0, 0).view(B * T, D)
-        # decode rows (B <= 8) go through the skinny GEMM (gemv.hip): at M = B the MFMA GEMM has
-        # one row tile and walks K latency-bound; prefill uses the MFMA GEMM
-        skinny = pos0 > 0 and C.gemv_supported(B * T, 4 * D)
 
         def lin(inp, w, b, epi, resid=None, ld=0, ln=None, am=None):
             """epi(LN(inp) @ w^T + b) with ``ln`` = a LayerNorm module applied first (fused into
@@ -163,7 +172,7 @@ class _GpuCache:
                 code = {"none": 0, "bias": 1, "gelu": 2, "resid": 3}[epi]
                 lw, lb = (bf(ln.weight), bf(ln.bias)) if ln is not None else (None, None)
                 if am is not None:
-                    return C.gemv(inp, bf(w), code, None, None, ld, lw, lb, eps, am[0], am[1], am[2])
+                    return C.gemv(inp, bf(w), code, None, None, ld, lw, lb, eps, am[0], am[1])
                 return C.gemv(inp, bf(w), code, bf(b) if b is not None else None, resid, ld, lw, lb, eps)
             if ln is not None:
                 inp, _, _ = C.layernorm_fwd(inp, bf(ln.weight), bf(ln.bias), eps)
@@ -185,13 +194,10 @@ class _GpuCache:
             u = lin(x, mm.c_fc.weight, mm.c_fc.bias, "gelu", ln=blk.ln_2)
             x = lin(u, mm.c_proj.weight, mm.c_proj.bias, "resid", resid=x)
         last = x.view(B, T, D)[:, -1].contiguous()
-        V = cfg.vocab_size
-        am = None
-        if greedy is not None and skinny and V > 8192:
-            am = (greedy[0].view(B), greedy[1], greedy[2])
+        am = (part, pos_dev) if part is not None else None
         logits = lin(last, m.lm_head.weight, None, "none", ld=(V + 7) // 8 * 8, ln=tr.ln_f, am=am)
-        if greedy is not None and am is None:  # small vocab (no fused argmax): same effect in torch
-            tok, pd, seq = greedy
+        if greedy is not None and part is None:  # small vocab (no fused argmax): same in torch
+            tok, pd, seq, _ = greedy
             nxt = logits[:, :V].argmax(-1)
             tok.view(B).copy_(nxt)
             seq.index_copy_(1, (pd.long() + 1), nxt.view(B, 1))
@@ -228,32 +234,54 @@ class _GpuCache:
 
     def greedy(self, tok, pos, n):
         """n greedy decode steps starting with token ``tok`` [B, 1] at position ``pos``: the captured
-        step takes its input token and position from device buffers that its own LM-head kernel
-        overwrites (fused argmax), so the n replays are queued back to back without a host round
+        step takes its input token and position from device buffers that its own kernels advance
+        (fused argmax, see ``_run``), so the n replays are queued back to back without a host round
         trip.  Returns the n new tokens [B, n] (positions pos + 1 .. pos + n)."""
         assert pos + n <= self.tmax
         B = tok.shape[0]
         self._fresh()
         g = getattr(self, "_ggraph", None)
+        cfg = self.model.config
+        fused = self.C.gemv_supported(B, 4 * cfg.n_embed) and cfg.vocab_size > 8192
         if g is None:
             dev = tok.device
             g = {"tok": tok.clone(), "pos": torch.full((1,), pos, dtype=torch.int32, device=dev),
-                 "seq": torch.zeros(B, self.tmax + 1, dtype=torch.long, device=dev)}
-            self._run(g["tok"], max(pos, 1), g["pos"], (g["tok"], g["pos"], g["seq"]))  # warm-up:
-            self._ggraph = g  # workspaces are allocated outside the capture
+                 "seq": torch.zeros(B, self.tmax + 1, dtype=torch.long, device=dev),
+                 "part": (torch.zeros(B, self.C.gemv_argmax_groups(cfg.vocab_size), dtype=torch.long,
+                                      device=dev) if fused else None)}
+            self._ggraph = g  # workspaces are allocated outside the capture (eager warm-up step)
+            self._greedy_seed(g, tok, pos)
+            self._run(g["tok"], max(pos, 1), g["pos"], (g["tok"], g["pos"], g["seq"], g["part"]))
         if _GRAPH_DECODE and "graph" not in g:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                self._run(g["tok"], max(pos, 1), g["pos"], (g["tok"], g["pos"], g["seq"]))
+                self._run(g["tok"], max(pos, 1), g["pos"], (g["tok"], g["pos"], g["seq"], g["part"]))
             g["graph"] = graph
-        g["tok"].copy_(tok)
-        g["pos"].fill_(pos)
+        self._greedy_seed(g, tok, pos)
         for _ in range(n):
             if _GRAPH_DECODE:
                 g["graph"].replay()
             else:
-                self._run(g["tok"], max(pos, 1), g["pos"], (g["tok"], g["pos"], g["seq"]))
-        return g["seq"][:, pos + 1:pos + 1 + n]
+                self._run(g["tok"], max(pos, 1), g["pos"], (g["tok"], g["pos"], g["seq"], g["part"]))
+        if g["part"] is None:
+            return g["seq"][:, pos + 1:pos + 1 + n]
+        # the last step's token is still in its LM-head keys: reduce them here (unsigned max =
+        # signed max after flipping the top bit; low word = 0xffffffff - column)
+        k = (g["part"] ^ _I64_MIN).max(dim=1).values ^ _I64_MIN
+        last = 0xFFFFFFFF - (k & 0xFFFFFFFF)
+        return torch.cat([g["seq"][:, pos + 1:pos + n], last.view(B, 1)], dim=1)
+
+    @staticmethod
+    def _greedy_seed(g, tok, pos):
+        """Point the greedy loop's device state at token ``tok`` [B, 1] at position ``pos``."""
+        g["tok"].copy_(tok)
+        g["pos"].fill_(pos)
+        if g["part"] is not None:  # keys that every real logit loses to, argmax = tok
+            g["part"].zero_()
+            g["part"][:, :1].copy_(-1 - tok)  # bits 0xffffffff_(0xffffffff - tok)
+
+
+_I64_MIN = -(1 << 63)
 
 
 def _weight_stamp(model):

@@ -108,8 +108,8 @@ def test_generate_graph_decode_matches_eager(monkeypatch):
 
 
 def test_greedy_device_loop_matches_host_argmax():
-    """The device-side greedy loop (LM-head GEMV with the fused argmax writing the next token and
-    position) == the logits step followed by torch.argmax, token for token; vocab > 8192 takes
+    """The device-side greedy loop (LM-head GEMV leaving per-workgroup argmax keys that the next
+    step's embedding kernel reduces into its token) == the logits step followed by torch.argmax, token for token; vocab > 8192 takes
     the fused path.  Also: generate() across the block_size window and a second call that reuses
     the cached decode state."""
     from mingpt_distributed_amd.models import generation as gen
