@@ -421,7 +421,7 @@ std::vector<at::Tensor> attention_fwd(const at::Tensor& qkv, int64_t B, int64_t 
 
 at::Tensor attention_bwd(const at::Tensor& qkv, const at::Tensor& out, const at::Tensor& dout,
                          const at::Tensor& lse, const at::Tensor& mask, int64_t B, int64_t T,
-                         int64_t H, double p, int64_t seed) {
+                         int64_t H, double p, int64_t seed, const c10::optional<at::Tensor>& dbias) {
   CHECK_BF16(qkv); CHECK_BF16(out); CHECK_BF16(dout); CHECK_F32(lse);
   CHECK_CONTIG(qkv); CHECK_CONTIG(out); CHECK_CONTIG(dout);
   const int64_t D3 = qkv.size(-1), D = D3 / 3, hd = D / H;
@@ -442,8 +442,14 @@ at::Tensor attention_bwd(const at::Tensor& qkv, const at::Tensor& out, const at:
                 "attention_bwd: dropout mask from attention_fwd required when p > 0");
     mp = reinterpret_cast<const uint32_t*>(mask.data_ptr<int>());
   }
+  float* db = nullptr;
+  if (dbias.has_value() && dbias->defined()) {
+    CHECK_F32(*dbias); CHECK_CONTIG(*dbias);
+    TORCH_CHECK(dbias->numel() == D3, "attention_bwd: dbias must be fp32 [3D]");
+    db = fp(*dbias);
+  }
   mg::attention_bwd(bp(qkv), bp(out), bp(dout), fp(lse), mp, fp(delta), fp(dq), bp(dqkv), (int)B,
-                    (int)T, (int)H, (int)hd, (float)p, (uint64_t)seed, cur_stream());
+                    (int)T, (int)H, (int)hd, (float)p, (uint64_t)seed, cur_stream(), db);
   return dqkv;
 }
 
@@ -553,7 +559,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_get_variant", &mg::gemm_get_variant);
   m.def("attention_set_bwd_mode", &mg::attention_set_bwd_mode);
   m.def("attention_fwd", &attention_fwd);
-  m.def("attention_bwd", &attention_bwd);
+  m.def("attention_bwd", &attention_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"),
+        py::arg("mask"), py::arg("B"), py::arg("T"), py::arg("H"), py::arg("p"), py::arg("seed"),
+        py::arg("dbias") = py::none());
   m.def("gemv", &gemv, py::arg("x"), py::arg("W"), py::arg("epi"), py::arg("bias") = py::none(),
         py::arg("resid") = py::none(), py::arg("ldy") = 0, py::arg("lnw") = py::none(),
         py::arg("lnb") = py::none(), py::arg("eps") = 1e-5, py::arg("am_part") = py::none(),

@@ -34,6 +34,7 @@ struct AttnArgs {
   float scale_log2;    // log2(e) / sqrt(hd)
   uint32_t thr;        // 8-bit keep threshold: keep iff random byte >= thr (0 = no dropout)
   float dscale;        // 1 / (1 - thr/256)
+  float* dbias;        // bwd key-block mode: += column sums of dK / dV into [D, 3D) (qkv bias grad), or null
 };
 
 MG_DEVICE float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }  // v_exp_f32, no denorm fixup

@@ -105,9 +105,11 @@ void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, uint32_t* dmask, 
 // slots of dqkv
 size_t attention_bwd_workspace_floats(int B, int T, int H, int hd);
 void attention_set_bwd_mode(int mode);  // 0 auto, 1 persistent (b, h) workgroups, 2 key-block partials
+// dbias (fp32 [3D] or null): += the column sums of dqkv (the qkv bias gradient), fused into the
+// backward kernels where the schedule allows
 void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse,
                    const uint32_t* dmask, float* delta, float* dq, bf16_t* dqkv, int B, int T, int H,
-                   int hd, float p, uint64_t seed, hipStream_t stream);
+                   int hd, float p, uint64_t seed, hipStream_t stream, float* dbias = nullptr);
 
 // one decode step: appends K/V of qkv_new [B, 3D] at row pos of cache [B, Tmax, 3D]; out [B, D]
 void attention_decode(const bf16_t* qkv_new, bf16_t* cache, bf16_t* out, int B, int H, int hd,

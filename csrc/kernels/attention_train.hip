@@ -373,6 +373,22 @@ struct Stager {
   }
 };
 
+// Transpose-reduce over the 32 lanes of each half-wave: each step halves the values a lane keeps
+// (the lane's bit M picks the half) and adds its partner's copy of that half, so a lane ends with
+// NV / 32 sums, value index NV / 32 * (lane & 31) + j for v[j] -- 31 NV / 32 shuffles instead of
+// 5 NV for a full butterfly per value.
+template <int M, int C, int NV>
+MG_DEVICE void tr_reduce32(float (&v)[NV], int lane) {
+  const bool hi = lane & M;
+#pragma unroll
+  for (int i = 0; i < C / 2; ++i) {
+    const float send = hi ? v[i] : v[i + C / 2];
+    const float keep = hi ? v[i + C / 2] : v[i];
+    v[i] = keep + __shfl_xor(send, M, 64);
+  }
+  if constexpr (M > 1) tr_reduce32<M / 2, C / 2, NV>(v, lane);
+}
+
 // Key-block-parallel backward, one workgroup per (b, h) sweeping its key blocks in order.
 //  * KW waves = KB = 32 KW keys per block (K pre-scaled by log2(e)/sqrt(hd) in LDS); each wave
 //    keeps its 32 keys' V rows (the dP~ B operand) and dK^T / dV^T accumulators (keys on the lane)
@@ -697,6 +713,40 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
           }
         }
     }
+    if constexpr (!PERSIST) {
+      if (a.dbias) {
+        // qkv bias gradient, K and V columns: this block's keys summed in registers (lanes), the
+        // KW waves through LDS (free: every read of the last tile is behind its final barrier),
+        // then one fp32 atomic per column -- the separate 300 MB column-sum pass over dqkv is gone
+        constexpr int NV = 32 * NO;  // this lane's dK then dV values
+        float v[NV];
+        const bool kv = mykey < a.T;
+        const float sc = a.scale_log2 * 0.6931471805599453f;
+        const float vs = a.thr ? a.dscale : 1.f;
+#pragma unroll
+        for (int n = 0; n < NO; ++n)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            v[n * 16 + r] = kv ? dk[n][r] * sc : 0.f;
+            v[16 * NO + n * 16 + r] = kv ? dv[n][r] * vs : 0.f;
+          }
+        tr_reduce32<16, NV, NV>(v, lane);
+        float* red = reinterpret_cast<float*>(smem);  // [KW][NO][64]
+#pragma unroll
+        for (int j = 0; j < NO; ++j) red[(w * NO + j) * 64 + lane] = v[j];
+        __syncthreads();
+        for (int t = threadIdx.x; t < 64 * NO; t += NT) {
+          const int ln = t & 63, j = t >> 6;
+          float s = 0.f;
+#pragma unroll
+          for (int ww = 0; ww < KW; ++ww) s += red[(ww * NO + j) * 64 + ln];
+          const int idx = NO * (ln & 31) + j;  // value index (tr_reduce32)
+          const int tk = idx / (16 * NO), n = (idx % (16 * NO)) / 16, r = idx % 16;
+          const int d = n * 32 + 8 * (r >> 2) + 4 * (ln >> 5) + (r & 3);
+          if (d < a.hd) atomicAdd(a.dbias + (1 + tk) * a.D + hh * a.hd + d, s);
+        }
+      }
+    }
   }
 }
 
@@ -730,6 +780,55 @@ __global__ __launch_bounds__(256) void attn_dq_finalize_kernel(const float* __re
   }
   const float f[8] = {x0.x * sc, x0.y * sc, x0.z * sc, x0.w * sc, x1.x * sc, x1.y * sc, x1.z * sc, x1.w * sc};
   st16_nt(dqkv + (long)r * 3L * D + c, pack8(f));
+}
+
+// the same, fused with the qkv bias gradient's Q columns: thread = (row group g, 8-column chunk);
+// RPB row groups sweep the rows, keep 8 column sums of the stored (rounded) dQ, fold them through
+// LDS and add one fp32 atomic per column per block.  blockDim = (D / 8) * RPB, LDS = RPB * D floats.
+__global__ __launch_bounds__(1024) void attn_dq_finalize_bias_kernel(const float* __restrict__ dq,
+                                                                     bf16_t* __restrict__ dqkv,
+                                                                     float* __restrict__ dbias, int rows,
+                                                                     int D, int T, int KB, long part,
+                                                                     float sc) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [RPB][D]
+  const int cpb = D / 8, rpb = blockDim.x / cpb;
+  const int g = threadIdx.x / cpb, c = (threadIdx.x % cpb) * 8;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int r = blockIdx.x * rpb + g; r < rows; r += gridDim.x * rpb) {
+    const int np = (r % T) / KB + 1;
+    const float* src = dq + (long)r * D + c;
+    float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
+    for (int k = 0; k < np; k += 4) {
+      float4 y[4][2];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool ok = k + u < np;
+        const float* s = src + (long)(ok ? k + u : k) * part;
+        const uint4 a0 = ok ? ld16_nt(s) : make_uint4(0, 0, 0, 0), a1 = ok ? ld16_nt(s + 4) : make_uint4(0, 0, 0, 0);
+        y[u][0] = make_float4(__uint_as_float(a0.x), __uint_as_float(a0.y), __uint_as_float(a0.z), __uint_as_float(a0.w));
+        y[u][1] = make_float4(__uint_as_float(a1.x), __uint_as_float(a1.y), __uint_as_float(a1.z), __uint_as_float(a1.w));
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        x0.x += y[u][0].x; x0.y += y[u][0].y; x0.z += y[u][0].z; x0.w += y[u][0].w;
+        x1.x += y[u][1].x; x1.y += y[u][1].y; x1.z += y[u][1].z; x1.w += y[u][1].w;
+      }
+    }
+    const float f[8] = {x0.x * sc, x0.y * sc, x0.z * sc, x0.w * sc, x1.x * sc, x1.y * sc, x1.z * sc, x1.w * sc};
+    const uint4 o = pack8(f);
+    st16_nt(dqkv + (long)r * 3L * D + c, o);
+    const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cs[k] += bf2f((ow[k >> 1] >> (16 * (k & 1))) & 0xffffu);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[g * D + c + k] = cs[k];
+  __syncthreads();
+  for (int col = threadIdx.x; col < D; col += blockDim.x) {
+    float s = 0.f;
+    for (int i = 0; i < rpb; ++i) s += red[i * D + col];
+    atomicAdd(dbias + col, s);
+  }
 }
 
 template <int NKS, int KW>
@@ -842,7 +941,7 @@ void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, uint32_t* dmask, 
 
 void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse,
                    const uint32_t* dmask, float* delta, float* dq, bf16_t* dqkv, int B, int T, int H,
-                   int hd, float p, uint64_t seed, hipStream_t stream) {
+                   int hd, float p, uint64_t seed, hipStream_t stream, float* dbias) {
   (void)seed;
   AttnArgs a{};
   a.B = B; a.T = T; a.H = H; a.hd = hd; a.D = H * hd;
@@ -853,6 +952,12 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
   a.dq = dq; a.dqkv = dqkv; a.dmask = dmask;
   const bool persistent = bwd_persistent(T, hd);
   a.dq_part = persistent ? 0 : (long)B * T * H * hd;
+  // qkv bias gradient fused into the key-block kernel (K / V columns) and the dQ finalize (Q
+  // columns); the persistent schedule and very wide rows take the separate column-sum pass
+  const int D = H * hd;
+  const int cpb = D / 8, rpb = cpb <= 768 ? std::max(1, 768 / cpb) : 0;
+  const bool fuse_db = dbias && !persistent && rpb > 0;
+  a.dbias = fuse_db ? dbias : nullptr;
   int lg = 0;
   while ((8 << lg) < hd) ++lg;
   const long nthreads = (long)B * T * H << lg;
@@ -865,11 +970,16 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
     case 6: launch_bwd<6, 4>(a, stream); break;
     default: launch_bwd<8, 4>(a, stream); break;
   }
-  if (!persistent) {
+  if (fuse_db) {
+    const int grid = std::min(num_cus(), cdiv(B * T, rpb));
+    attn_dq_finalize_bias_kernel<<<grid, cpb * rpb, rpb * D * 4, stream>>>(
+        dq, dqkv, dbias, B * T, D, T, bwd_keys_per_block(hd), a.dq_part, 0.6931471805599453f);
+  } else if (!persistent) {
     const long n8 = (long)B * T * (H * hd / 8);
     attn_dq_finalize_kernel<<<(unsigned)cdiv(n8, 256), 256, 0, stream>>>(
         dq, dqkv, B * T, H * hd, T, bwd_keys_per_block(hd), a.dq_part, 0.6931471805599453f);
   }
+  if (dbias && !fuse_db) bias_grad(dqkv, dbias, (long)B * T, 3 * D, stream);
 }
 
 void attention_set_bwd_mode(int mode) { g_bwd_mode = mode; }

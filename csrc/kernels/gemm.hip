@@ -247,10 +247,15 @@ MG_DEVICE void store8(bf16_t* p, uint4 v, int valid) {
     if (e < valid) p[e] = (uint16_t)(w[e >> 1] >> (16 * (e & 1)));
 }
 
+// EPI 4 bias gradient in the staged epilogue: a lane's 8-column piece index e % PR is the same in
+// every pass when PR divides 64, so each lane keeps 8 running column sums of the rounded outputs
+template <class CF>
+constexpr bool staged_dbias() { return 64 % (CF::WTN / 8) == 0; }
+
 // LDS -> global half of the staged epilogue for rows [mr, mr + 16 CHF) of the wave tile
 template <class CF, int EPI, bool F32, int S, int CHF, int PR, int IT, bool CHECK>
 MG_DEVICE void staged_rows(const GemmArgs& args, const char* st, const uint4 (&sd)[F32 ? IT : 1], int mr,
-                           int nw, int nlim, int lane) {
+                           int nw, int nlim, int lane, float (&cs)[8]) {
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     const int e = it * 64 + lane, r = e / PR, p = e % PR;
@@ -268,6 +273,13 @@ MG_DEVICE void staged_rows(const GemmArgs& args, const char* st, const uint4 (&s
         v[k] = EPI == 3 ? v[k] + s : v[k] * s;
       }
       y = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+      if constexpr (EPI == 4 && staged_dbias<CF>()) {  // column sums of the stored (rounded) values
+        const bool ok = !CHECK || m < args.M;
+        const uint32_t o[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          cs[k] += (ok && (!CHECK || n + k < nlim)) ? bf2f((o[k >> 1] >> (16 * (k & 1))) & 0xffffu) : 0.f;
+      }
     } else {
       y = *reinterpret_cast<const uint4*>(row + p * 16);
     }
@@ -320,6 +332,7 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
   const bf16_t* __restrict__ side = EPI == 3 ? args.resid : args.aux;
   const uint32_t dkey = EPI == 3 ? rowdrop_key(eff_seed(args.seed, args.sofs)) : 0u;  // dropout key
   const bool full = nw + CF::WTN <= nlim && mw + CF::WTM <= args.M;  // wave-uniform: no per-piece checks
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // EPI 4 + dbias: this lane's column sums
 #pragma unroll
   for (int c = 0; c < CF::FM / CHF; ++c) {
     // side inputs of this pass first: their latency hides under the LDS staging
@@ -366,9 +379,32 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (full) staged_rows<CF, EPI, F32, S, CHF, PR, IT, false>(args, st, sd, mw + c * CHF * 16, nw, nlim, lane);
-    else staged_rows<CF, EPI, F32, S, CHF, PR, IT, true>(args, st, sd, mw + c * CHF * 16, nw, nlim, lane);
+    if (full) staged_rows<CF, EPI, F32, S, CHF, PR, IT, false>(args, st, sd, mw + c * CHF * 16, nw, nlim, lane, cs);
+    else staged_rows<CF, EPI, F32, S, CHF, PR, IT, true>(args, st, sd, mw + c * CHF * 16, nw, nlim, lane, cs);
     asm volatile("" ::: "memory");  // the next pass's LDS writes stay behind these reads
+  }
+  if constexpr (EPI == 4 && staged_dbias<CF>()) {
+    if (args.dbias) {  // kernel argument: uniform over the workgroup
+      // lanes sharing a piece index (lane % PR) fold by shuffles, the NWM row-waves through LDS,
+      // then one atomic per tile column with 64 contiguous floats per wave-instruction
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int o = PR; o < 64; o <<= 1) cs[k] += __shfl_xor(cs[k], o, 64);
+      float* red = reinterpret_cast<float*>(smem);  // [NWM][BN], over the staging regions
+      __syncthreads();  // every wave's staged reads are done
+      if (lane < PR) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) red[wm * CF::BN + wn * CF::WTN + lane * 8 + k] = cs[k];
+      }
+      __syncthreads();
+      for (int c = threadIdx.x; c < CF::BN; c += CF::NT) {
+        float t = 0.f;
+#pragma unroll
+        for (int r = 0; r < CF::NWM; ++r) t += red[r * CF::BN + c];
+        if (n0 + c < args.N) atomicAdd(args.dbias + n0 + c, t);
+      }
+    }
   }
 }
 
@@ -378,7 +414,7 @@ template <class CF, int EPI, bool OUTF32, int LDSW>
 MG_DEVICE void epilogue(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int m0, int n0, int wm,
                         int wn, int wid, int lane, char* smem) {
   if constexpr (!OUTF32) {
-    if (EPI != 4 || !args.dbias) {
+    if (EPI != 4 || !args.dbias || staged_dbias<CF>()) {
       epilogue_staged<CF, EPI, LDSW>(args, acc, m0, n0, wm, wn, wid, lane, smem);
       return;
     }

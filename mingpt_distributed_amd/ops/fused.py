@@ -52,6 +52,14 @@ def _bf16(t: torch.Tensor) -> torch.Tensor:
 _DGRAD_BLAS = os.environ.get("MINGPT_DGRAD_BLAS", "0") == "1"
 _WGRAD_BLAS = os.environ.get("MINGPT_WGRAD_BLAS", "0") == "1"
 _QKV_BLAS = os.environ.get("MINGPT_QKV_BLAS", "0") == "1"
+# The MLP fc bias gradient summed inside the fc2 data-gradient GEMM's staged epilogue (one add per
+# stored element, one atomic per tile column) instead of a separate 400 MB column-sum pass over
+# dpre.  MINGPT_FC_DBIAS_FUSED=0 restores the separate bias_grad kernel.
+_FC_DBIAS_FUSED = os.environ.get("MINGPT_FC_DBIAS_FUSED", "1") == "1"
+# The qkv bias gradient summed inside the attention backward (dK / dV columns per key block in
+# registers, dQ columns in the dQ finalize) instead of a separate 300 MB pass over dqkv.
+# MINGPT_QKV_DBIAS_FUSED=0 restores the separate bias_grad kernel.
+_QKV_DBIAS_FUSED = os.environ.get("MINGPT_QKV_DBIAS_FUSED", "1") == "1"
 
 
 # Library calls cost more host time per launch than the extension's; small models (gpt-mini:
@@ -160,9 +168,12 @@ class TransformerBlockFn(_EngineFn):
             dz = dx2
             C.bias_grad(dz, g[id(bp)][0])
         _wgrad(dz, u, g[id(wp)][0])
-        dpre = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=gd)
+        if _FC_DBIAS_FUSED:  # fc bias gradient: column sums of dpre in the GELU' epilogue
+            dpre = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=gd, dbias=g[id(bfc)][0])
+        else:
+            dpre = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=gd)
+            C.bias_grad(dpre, g[id(bfc)][0])
         _wgrad(dpre, h2, g[id(wfc)][0])
-        C.bias_grad(dpre, g[id(bfc)][0])  # separate pass: cheaper than column sums in the epilogue
         dh2 = _dgrad(dpre, wfc)
         dx1 = C.layernorm_bwd(dh2, x1, ln2w, mean2, rstd2, g[id(ln2w)][0], g[id(ln2b)][0], dx2)
         # ---- attention: x1 = x + drop(attn(h Wqkv^T + bqkv) Wo^T + bo)
@@ -173,9 +184,13 @@ class TransformerBlockFn(_EngineFn):
             C.bias_grad(dz, g[id(bo)][0])
         _wgrad(dz, y, g[id(wo)][0])
         dy = _dgrad(dz, wo)
-        dqkv = C.attention_bwd(qkv, y, dy, lse, amask, B, T, H, float(p_attn), ctx.seeds[0])
+        if _QKV_DBIAS_FUSED:  # qkv bias gradient summed inside the attention backward
+            dqkv = C.attention_bwd(qkv, y, dy, lse, amask, B, T, H, float(p_attn), ctx.seeds[0],
+                                   g[id(bqkv)][0])
+        else:
+            dqkv = C.attention_bwd(qkv, y, dy, lse, amask, B, T, H, float(p_attn), ctx.seeds[0])
+            C.bias_grad(dqkv, g[id(bqkv)][0])
         _wgrad(dqkv, h, g[id(wqkv)][0])
-        C.bias_grad(dqkv, g[id(bqkv)][0])
         dh = _dgrad(dqkv, wqkv)
         dx = C.layernorm_bwd(dh, x, ln1w, mean1, rstd1, g[id(ln1w)][0], g[id(ln1b)][0], dx1)
         outs = [finish(prm, *g[id(prm)]) for prm in ctx.params]

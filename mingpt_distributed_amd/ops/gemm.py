@@ -86,29 +86,32 @@ def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, *, epi: str = "none",
                dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dX = dY @ W (W [N_out, N_in] as stored by nn.Linear).  Block shapes run NN straight from the
     stored weight (the W4 kernel's transposing LDS reads; no per-step transposed copy:
-    bench/dgrad_nn_vs_nt.py); a long reduction (the LM head's K = vocab) or ``dbias`` runs NT
-    against W^T, where the 128x96-wave W4 tile applies.  With ``epi="gelu_bwd"`` and ``dbias``, the
-    bias gradient of the result is accumulated in the epilogue."""
-    if _DGRAD_NN and wt is None and dbias is None and dy.shape[1] < 8192 and w.shape[0] == dy.shape[1]:
-        return gemm_nn(dy, w, epi=epi, aux=aux)
+    bench/dgrad_nn_vs_nt.py); a long reduction (the LM head's K = vocab) runs NT against W^T, where
+    the 128x96-wave W4 tile applies.  With ``epi="gelu_bwd"`` and ``dbias`` (fp32 [N_in]), the
+    column sums of the result (the next bias gradient) are accumulated in the epilogue."""
+    if _DGRAD_NN and wt is None and dy.shape[1] < 8192 and w.shape[0] == dy.shape[1]:
+        return gemm_nn(dy, w, epi=epi, aux=aux, dbias=dbias)
     if wt is None:
         wt = transpose(w, dy.shape[1])
     return gemm_nt(dy, wt, epi=epi, aux=aux, dbias=dbias)
 
 
 def gemm_nn(a: torch.Tensor, b: torch.Tensor, *, epi: str = "none",
-            aux: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """C = A @ B (B row-major [K, N]); ``gelu_bwd`` multiplies by ``aux`` (a stored GELU')."""
+            aux: Optional[torch.Tensor] = None, dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """C = A @ B (B row-major [K, N]); ``gelu_bwd`` multiplies by ``aux`` (a stored GELU') and,
+    with ``dbias`` (fp32 [N]), adds the column sums of the stored C into it (staged epilogue)."""
     _check2d(a, "A")
     _check2d(b, "B")
     M, K = a.shape
     N = b.shape[1]
     c = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
     code = {"none": EPI_NONE, "gelu_bwd": EPI_GELU_BWD}[epi]
+    if dbias is not None and code != EPI_GELU_BWD:
+        raise ValueError("gemm_nn: dbias is fused only into the gelu_bwd epilogue")
     chunks = _row_chunks(M, 2 * K, 2 * N)
     for r0, r1 in chunks:
         sl = (lambda t: t if t is None or len(chunks) == 1 else t[r0:r1])
-        ext().gemm(sl(a), b, sl(c), 1, code, None, sl(aux), None, 0.0, 0, r1 - r0, N)
+        ext().gemm(sl(a), b, sl(c), 1, code, None, sl(aux), None, 0.0, 0, r1 - r0, N, dbias)
     return c
 
 

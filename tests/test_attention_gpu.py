@@ -52,6 +52,30 @@ def test_attention_fwd_bwd(B, T, H, hd):
     torch.testing.assert_close(dqkv.float(), g, atol=3e-2 * max(1.0, scale / 4), rtol=5e-2)
 
 
+@pytest.mark.parametrize("B,T,H,hd,p", [(2, 1024, 2, 64, 0.0), (2, 1024, 2, 64, 0.1), (1, 520, 2, 80, 0.0),
+                                        (1, 300, 2, 128, 0.1), (2, 200, 2, 96, 0.0), (1, 777, 1, 24, 0.0),
+                                        (2, 128, 3, 64, 0.0)])
+def test_attention_bwd_fused_bias_grad(B, T, H, hd, p):
+    """attention_bwd(..., dbias) adds the column sums of dqkv (the qkv bias gradient) into dbias:
+    fused into the key-block kernel (dK / dV) and the dQ finalize (dQ), or a separate pass in the
+    persistent schedule.  Equal to the sums of the returned dqkv, and dqkv itself unchanged."""
+    C = ext()
+    torch.manual_seed(1)
+    D = H * hd
+    qkv = torch.randn(B * T, 3 * D, device=DEV).to(torch.bfloat16)
+    out, lse, mask = C.attention_fwd(qkv, B, T, H, p, 7)
+    dout = torch.randn(B * T, D, device=DEV).to(torch.bfloat16)
+    plain = C.attention_bwd(qkv, out, dout, lse, mask, B, T, H, p, 7)
+    db = torch.full((3 * D,), 0.5, device=DEV)
+    dqkv = C.attention_bwd(qkv, out, dout, lse, mask, B, T, H, p, 7, db)
+    torch.testing.assert_close(dqkv, plain, atol=0, rtol=0)
+    ref = 0.5 + dqkv.float().sum(0)
+    # dK / dV are summed before their bf16 rounding (independent errors of <= 2^-9 relative per
+    # element): ~6 sigma of that rounding noise over the column
+    tol = 6e-3 * dqkv.float().pow(2).sum(0).max().item() ** 0.5 + 1e-2
+    torch.testing.assert_close(db, ref, atol=tol, rtol=2e-3)
+
+
 def test_attention_causality():
     """Perturbing token j must not change outputs at positions < j (reference defect D4)."""
     C = ext()

@@ -121,13 +121,19 @@ def test_dgrad_nt(M, Nout, Nin):
     _check(G.gemm_dgrad(dy, w, epi="gelu_bwd", aux=gd), ref * gd.float(), Nout)
 
 
-def test_dgrad_gelu_bwd_bias_grad():
-    """The GELU' dgrad epilogue also accumulates the output's column sums (fc bias gradient)."""
-    M, Nout, Nin = 1000, 768, 3072
-    dy, w, gd = _bf(M, Nout, seed=21), _bf(Nout, Nin, seed=22), _bf(Nin, seed=23).repeat(M, 1)
+@pytest.mark.parametrize("M", [1000, 8192])  # partial tiles (T128 kernel) / the W4 kernel
+@pytest.mark.parametrize("nt", [False, True])  # NN from the stored weight / NT against W^T
+def test_dgrad_gelu_bwd_bias_grad(M, nt):
+    """The GELU' dgrad epilogue also accumulates the output's column sums (fc bias gradient) in
+    its LDS-staged form: equal to the sums of the stored bf16 output."""
+    Nout, Nin = 768, 3072
+    dy, w, gd = _bf(M, Nout, seed=21), _bf(Nout, Nin, seed=22), _bf(M, Nin, seed=23)
     db = torch.ones(Nin, device=DEV)
-    out = G.gemm_dgrad(dy, w, epi="gelu_bwd", aux=gd.contiguous(), dbias=db)
-    torch.testing.assert_close(db, 1 + out.float().sum(0), atol=5e-1, rtol=1e-2)
+    wt = G.transpose(w, Nout) if nt else None
+    out = G.gemm_dgrad(dy, w, epi="gelu_bwd", aux=gd.contiguous(), dbias=db, wt=wt)
+    ref = (dy.float() @ w.float()) * gd.float()
+    _check(out, ref, Nout)
+    torch.testing.assert_close(db, 1 + out.float().sum(0), atol=5e-2 * (M / 1000) ** 0.5, rtol=1e-3)
 
 
 def test_row_chunked_launches_match(monkeypatch):
