@@ -69,7 +69,7 @@ MG_DEVICE void gemv_argmax(const GemvArgmax& am, const unsigned long long (&key)
   if (blockIdx.x == 0 && threadIdx.x == 0) *am.pos += 1;  // nothing else in this kernel reads it
 }
 
-template <int B, int LPR>
+template <int B, int LPR, bool NTW>
 __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ x,
                                                    const bf16_t* __restrict__ W,
                                                    bf16_t* __restrict__ y, int N, int K, long ldy,
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ x,
 #pragma unroll
     for (int u = 0; u < NPF; ++u) {
       const int c = j * 8 + u * STRIDE;
-      wpf[u] = c < K ? ld16_nt(wr + c) : make_uint4(0, 0, 0, 0);
+      wpf[u] = c < K ? (NTW ? ld16_nt(wr + c) : ld16(wr + c)) : make_uint4(0, 0, 0, 0);
     }
   }
   if (lnw) {
@@ -247,7 +247,8 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ x,
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int c = seg * 1024 + j * 8 + u * STRIDE;
-        r[u] = c < K ? ld16_nt(wr + j * 8 + u * STRIDE) : make_uint4(0, 0, 0, 0);
+        r[u] = c < K ? (NTW ? ld16_nt(wr + j * 8 + u * STRIDE) : ld16(wr + j * 8 + u * STRIDE))
+                     : make_uint4(0, 0, 0, 0);
       }
     };
     uint4 cur[8], nxt[8];
@@ -306,6 +307,16 @@ int gemv_wide_cap() {
   return cap;
 }
 int gemv_grid(int N) { return N > 8192 ? min(cdiv(N, 16), gemv_wide_cap()) : cdiv(N, 4); }
+// weight loads non-temporal (default) or default cache policy (MINGPT_GEMV_NT=0): the decode step
+// re-reads the same ~250 MB of GPT-2 weights every token, about the Infinity Cache's size
+bool gemv_nt_weights() {
+  static int nt = -1;
+  if (nt < 0) {
+    const char* e = getenv("MINGPT_GEMV_NT");
+    nt = e ? atoi(e) != 0 : 1;
+  }
+  return nt != 0;
+}
 // argmax partials: one 8-byte key per (row, workgroup)
 
 void gemv(const bf16_t* x, const bf16_t* W, bf16_t* y, int B, int N, int K, long ldy, const bf16_t* bias,
@@ -317,12 +328,17 @@ void gemv(const bf16_t* x, const bf16_t* W, bf16_t* y, int B, int N, int K, long
   const bool wide = N > 8192;
   const int grid = gemv_grid(N);
   const GemvArgmax amv = am ? *am : GemvArgmax{nullptr, nullptr};
-#define MG_GEMV_CASE(b)                                                                                        \
-  case b:                                                                                                      \
-    if (wide)                                                                                                  \
-      gemv_kernel<b, 16><<<grid, 256, smem, stream>>>(x, W, y, N, K, ldy, bias, resid, epi, lnw, lnb, eps, amv); \
-    else                                                                                                       \
-      gemv_kernel<b, 64><<<grid, 256, smem, stream>>>(x, W, y, N, K, ldy, bias, resid, epi, lnw, lnb, eps, amv); \
+  const bool ntw = gemv_nt_weights();
+#define MG_GEMV_LAUNCH(b, lpr)                                                                                        \
+  if (ntw) gemv_kernel<b, lpr, true><<<grid, 256, smem, stream>>>(x, W, y, N, K, ldy, bias, resid, epi, lnw, lnb, eps, amv); \
+  else gemv_kernel<b, lpr, false><<<grid, 256, smem, stream>>>(x, W, y, N, K, ldy, bias, resid, epi, lnw, lnb, eps, amv);
+#define MG_GEMV_CASE(b)        \
+  case b:                      \
+    if (wide) {                \
+      MG_GEMV_LAUNCH(b, 16)    \
+    } else {                   \
+      MG_GEMV_LAUNCH(b, 64)    \
+    }                          \
     break;
   switch (B) {  // exact row counts: the kernel stages and writes exactly B rows
     MG_GEMV_CASE(1) MG_GEMV_CASE(2) MG_GEMV_CASE(3) MG_GEMV_CASE(4)
@@ -330,6 +346,7 @@ void gemv(const bf16_t* x, const bf16_t* W, bf16_t* y, int B, int N, int K, long
     default: break;
   }
 #undef MG_GEMV_CASE
+#undef MG_GEMV_LAUNCH
 }
 
 }  // namespace mg
