@@ -34,7 +34,7 @@ import torch
 # single-GPU torch-eager self-baseline at the SAME per-GPU batch, model, shape and dropout
 # (bench/baseline_torch.py: torch.autocast bf16, SDPA attention, torch AdamW, MI355X):
 # BASELINE.md "Self-baseline" table.
-BASELINE_TOK_S_PER_GPU = {16: 367595.5, 32: 413092.9, 64: 461947.8}
+BASELINE_TOK_S_PER_GPU = {16: 367595.5, 32: 413092.9, 64: 461947.8, 128: 470388.8}
 
 
 def _free_port() -> int:
@@ -63,8 +63,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64,
-                    help="sequences per GPU per step (64 x 1024 tokens: ~36 GB of the 288 GB HBM)")
+    ap.add_argument("--batch", type=int, default=128,
+                    help="sequences per GPU per step (128 x 1024 tokens: ~66 GB of the 288 GB HBM; "
+                         "B = 64 / 96 / 128 measured 989.7k / 998.1k / 1,009.4k tok/s on one box, "
+                         "profiles/round2_s8_batch_sweep.txt)")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--model", default="gpt2")
     ap.add_argument("--dropout", type=float, default=0.1)

@@ -478,11 +478,11 @@ at::Tensor gemv(const at::Tensor& x, const at::Tensor& W, int64_t epi, const c10
   mg::GemvArgmax am{};
   if (am_part.has_value()) {
     // greedy decode: the LM-head GEMV (N > 8192 rows) also leaves one argmax key per (row,
-    // workgroup) in am_part [B, gemv_grid(N)] (int64 storage of the unsigned keys) and advances
+    // workgroup) in am_part [B, gemv_grid(N, B)] (int64 storage of the unsigned keys) and advances
     // *am_pos; the next step's embedding_fwd(am_part=...) reduces the keys into the token
     TORCH_CHECK(N > 8192 && epi == 0, "gemv argmax: LM-head shape (N > 8192, no epilogue)");
     TORCH_CHECK(am_part->scalar_type() == at::kLong && am_part->is_cuda() && am_part->is_contiguous() &&
-                am_part->numel() == B * mg::gemv_grid((int)N), "gemv argmax: am_part int64 [B, gemv_argmax_groups(N)]");
+                am_part->numel() == B * mg::gemv_grid((int)N, (int)B), "gemv argmax: am_part int64 [B, gemv_argmax_groups(N, B)]");
     TORCH_CHECK(am_pos.has_value() && am_pos->scalar_type() == at::kInt && am_pos->is_cuda(),
                 "gemv argmax: am_pos int32 [1]");
     am.part = reinterpret_cast<unsigned long long*>(am_part->data_ptr<int64_t>());
@@ -566,7 +566,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("resid") = py::none(), py::arg("ldy") = 0, py::arg("lnw") = py::none(),
         py::arg("lnb") = py::none(), py::arg("eps") = 1e-5, py::arg("am_part") = py::none(),
         py::arg("am_pos") = py::none());
-  m.def("gemv_argmax_groups", [](int64_t N) { return (int64_t)mg::gemv_grid((int)N); });
+  m.def("gemv_argmax_groups", [](int64_t N, int64_t B) { return (int64_t)mg::gemv_grid((int)N, (int)B); },
+        py::arg("N"), py::arg("B"));
   m.def("gemv_supported", &mg::gemv_supported);
   m.def("attention_decode", &attention_decode, py::arg("qkv_new"), py::arg("cache"), py::arg("H"),
         py::arg("pos"), py::arg("pos_dev") = py::none());

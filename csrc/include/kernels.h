@@ -64,10 +64,10 @@ bool gemv_supported(int B, int K);
 // workgroups (first index on ties) is taken by the next step's embedding kernel (embedding_fwd
 // with am_part) or on the host after the last step.
 struct GemvArgmax {
-  unsigned long long* part;  // [B][gemv_grid(N)]
+  unsigned long long* part;  // [B][gemv_grid(N, B)]
   int* pos;                  // device position of the step (+1)
 };
-int gemv_grid(int N);
+int gemv_grid(int N, int B);  // workgroups of gemv() for N outputs at B rows (argmax key groups)
 void gemv(const bf16_t* x, const bf16_t* W, bf16_t* y, int B, int N, int K, long ldy, const bf16_t* bias,
           const bf16_t* resid, int epi, hipStream_t stream, const bf16_t* lnw = nullptr,
           const bf16_t* lnb = nullptr, float eps = 1e-5f, const GemvArgmax* am = nullptr);

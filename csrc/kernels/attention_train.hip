@@ -783,8 +783,9 @@ __global__ __launch_bounds__(256) void attn_dq_finalize_kernel(const float* __re
 }
 
 // the same, fused with the qkv bias gradient's Q columns: thread = (row group g, 8-column chunk);
-// RPB row groups sweep the rows, keep 8 column sums of the stored (rounded) dQ, fold them through
-// LDS and add one fp32 atomic per column per block.  blockDim = (D / 8) * RPB, LDS = RPB * D floats.
+// RPB row groups sweep the rows, keep 8 fp32 column sums of dQ, fold them through LDS and add one
+// fp32 atomic per column per block.  blockDim = (D / 8) * RPB, LDS = RPB * D floats; 4 blocks per
+// CU (one per CU left the partial loads too few in flight: 146 vs 104 us for the plain finalize).
 __global__ __launch_bounds__(1024) void attn_dq_finalize_bias_kernel(const float* __restrict__ dq,
                                                                      bf16_t* __restrict__ dqkv,
                                                                      float* __restrict__ dbias, int rows,
@@ -815,11 +816,9 @@ __global__ __launch_bounds__(1024) void attn_dq_finalize_bias_kernel(const float
       }
     }
     const float f[8] = {x0.x * sc, x0.y * sc, x0.z * sc, x0.w * sc, x1.x * sc, x1.y * sc, x1.z * sc, x1.w * sc};
-    const uint4 o = pack8(f);
-    st16_nt(dqkv + (long)r * 3L * D + c, o);
-    const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+    st16_nt(dqkv + (long)r * 3L * D + c, pack8(f));
 #pragma unroll
-    for (int k = 0; k < 8; ++k) cs[k] += bf2f((ow[k >> 1] >> (16 * (k & 1))) & 0xffffu);
+    for (int k = 0; k < 8; ++k) cs[k] += f[k];
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) red[g * D + c + k] = cs[k];
@@ -971,7 +970,7 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
     default: launch_bwd<8, 4>(a, stream); break;
   }
   if (fuse_db) {
-    const int grid = std::min(num_cus(), cdiv(B * T, rpb));
+    const int grid = std::min(4 * num_cus(), cdiv(B * T, rpb));
     attn_dq_finalize_bias_kernel<<<grid, cpb * rpb, rpb * D * 4, stream>>>(
         dq, dqkv, dbias, B * T, D, T, bwd_keys_per_block(hd), a.dq_part, 0.6931471805599453f);
   } else if (!persistent) {

@@ -306,7 +306,14 @@ int gemv_wide_cap() {
   }
   return cap;
 }
-int gemv_grid(int N) { return N > 8192 ? min(cdiv(N, 16), gemv_wide_cap()) : cdiv(N, 4); }
+// (B <= 2: twice the workgroups -- the LM head's 16-row blocks are then latency-, not
+// bandwidth-bound: 3,359 / 3,335 vs 3,319 / 3,302 tok/s at B = 1, equal at B = 8;
+// profiles/round2_s8_decode_gemv_policy_ab.jsonl)
+int gemv_grid(int N, int B) {
+  if (N <= 8192) return cdiv(N, 4);
+  const char* e = getenv("MINGPT_GEMV_WIDE_GRID");
+  return min(cdiv(N, 16), (e || B > 2) ? gemv_wide_cap() : 1024);
+}
 // weight loads non-temporal (default) or default cache policy (MINGPT_GEMV_NT=0): the decode step
 // re-reads the same ~250 MB of GPT-2 weights every token, about the Infinity Cache's size
 bool gemv_nt_weights() {
@@ -326,7 +333,7 @@ void gemv(const bf16_t* x, const bf16_t* W, bf16_t* y, int B, int N, int K, long
   // one row per wave (N / 4 workgroups) up to ~8k outputs; 4 rows per wave beyond (the LM head
   // already launches thousands of workgroups and re-stages x in each)
   const bool wide = N > 8192;
-  const int grid = gemv_grid(N);
+  const int grid = gemv_grid(N, B);
   const GemvArgmax amv = am ? *am : GemvArgmax{nullptr, nullptr};
   const bool ntw = gemv_nt_weights();
 #define MG_GEMV_LAUNCH(b, lpr)                                                                                        \

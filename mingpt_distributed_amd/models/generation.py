@@ -247,7 +247,7 @@ class _GpuCache:
             dev = tok.device
             g = {"tok": tok.clone(), "pos": torch.full((1,), pos, dtype=torch.int32, device=dev),
                  "seq": torch.zeros(B, self.tmax + 1, dtype=torch.long, device=dev),
-                 "part": (torch.zeros(B, self.C.gemv_argmax_groups(cfg.vocab_size), dtype=torch.long,
+                 "part": (torch.zeros(B, self.C.gemv_argmax_groups(cfg.vocab_size, B), dtype=torch.long,
                                       device=dev) if fused else None)}
             self._ggraph = g  # workspaces are allocated outside the capture (eager warm-up step)
             self._greedy_seed(g, tok, pos)

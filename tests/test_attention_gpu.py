@@ -70,8 +70,8 @@ def test_attention_bwd_fused_bias_grad(B, T, H, hd, p):
     dqkv = C.attention_bwd(qkv, out, dout, lse, mask, B, T, H, p, 7, db)
     torch.testing.assert_close(dqkv, plain, atol=0, rtol=0)
     ref = 0.5 + dqkv.float().sum(0)
-    # dK / dV are summed before their bf16 rounding (independent errors of <= 2^-9 relative per
-    # element): ~6 sigma of that rounding noise over the column
+    # dQ / dK / dV are summed before their bf16 rounding (independent errors of <= 2^-9 relative
+    # per element): ~6 sigma of that rounding noise over the column
     tol = 6e-3 * dqkv.float().pow(2).sum(0).max().item() ** 0.5 + 1e-2
     torch.testing.assert_close(db, ref, atol=tol, rtol=2e-3)
 

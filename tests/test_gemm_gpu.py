@@ -125,7 +125,8 @@ def test_dgrad_nt(M, Nout, Nin):
 @pytest.mark.parametrize("nt", [False, True])  # NN from the stored weight / NT against W^T
 def test_dgrad_gelu_bwd_bias_grad(M, nt):
     """The GELU' dgrad epilogue also accumulates the output's column sums (fc bias gradient) in
-    its LDS-staged form: equal to the sums of the stored bf16 output."""
+    its LDS-staged form: the fp32 values before their bf16 rounding, so equal to the sums of the
+    stored output up to that rounding noise."""
     Nout, Nin = 768, 3072
     dy, w, gd = _bf(M, Nout, seed=21), _bf(Nout, Nin, seed=22), _bf(M, Nin, seed=23)
     db = torch.ones(Nin, device=DEV)
@@ -133,7 +134,8 @@ def test_dgrad_gelu_bwd_bias_grad(M, nt):
     out = G.gemm_dgrad(dy, w, epi="gelu_bwd", aux=gd.contiguous(), dbias=db, wt=wt)
     ref = (dy.float() @ w.float()) * gd.float()
     _check(out, ref, Nout)
-    torch.testing.assert_close(db, 1 + out.float().sum(0), atol=5e-2 * (M / 1000) ** 0.5, rtol=1e-3)
+    tol = 6e-3 * out.float().pow(2).sum(0).max().item() ** 0.5 + 1e-2  # ~5 sigma of the rounding noise
+    torch.testing.assert_close(db, 1 + out.float().sum(0), atol=tol, rtol=1e-3)
 
 
 def test_row_chunked_launches_match(monkeypatch):
