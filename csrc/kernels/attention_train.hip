@@ -782,54 +782,6 @@ __global__ __launch_bounds__(256) void attn_dq_finalize_kernel(const float* __re
   st16_nt(dqkv + (long)r * 3L * D + c, pack8(f));
 }
 
-// the same, fused with the qkv bias gradient's Q columns: thread = (row group g, 8-column chunk);
-// RPB row groups sweep the rows, keep 8 fp32 column sums of dQ, fold them through LDS and add one
-// fp32 atomic per column per block.  blockDim = (D / 8) * RPB, LDS = RPB * D floats; 4 blocks per
-// CU (one per CU left the partial loads too few in flight: 146 vs 104 us for the plain finalize).
-__global__ __launch_bounds__(1024) void attn_dq_finalize_bias_kernel(const float* __restrict__ dq,
-                                                                     bf16_t* __restrict__ dqkv,
-                                                                     float* __restrict__ dbias, int rows,
-                                                                     int D, int T, int KB, long part,
-                                                                     float sc) {
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [RPB][D]
-  const int cpb = D / 8, rpb = blockDim.x / cpb;
-  const int g = threadIdx.x / cpb, c = (threadIdx.x % cpb) * 8;
-  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int r = blockIdx.x * rpb + g; r < rows; r += gridDim.x * rpb) {
-    const int np = (r % T) / KB + 1;
-    const float* src = dq + (long)r * D + c;
-    float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
-    for (int k = 0; k < np; k += 4) {
-      float4 y[4][2];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const bool ok = k + u < np;
-        const float* s = src + (long)(ok ? k + u : k) * part;
-        const uint4 a0 = ok ? ld16_nt(s) : make_uint4(0, 0, 0, 0), a1 = ok ? ld16_nt(s + 4) : make_uint4(0, 0, 0, 0);
-        y[u][0] = make_float4(__uint_as_float(a0.x), __uint_as_float(a0.y), __uint_as_float(a0.z), __uint_as_float(a0.w));
-        y[u][1] = make_float4(__uint_as_float(a1.x), __uint_as_float(a1.y), __uint_as_float(a1.z), __uint_as_float(a1.w));
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        x0.x += y[u][0].x; x0.y += y[u][0].y; x0.z += y[u][0].z; x0.w += y[u][0].w;
-        x1.x += y[u][1].x; x1.y += y[u][1].y; x1.z += y[u][1].z; x1.w += y[u][1].w;
-      }
-    }
-    const float f[8] = {x0.x * sc, x0.y * sc, x0.z * sc, x0.w * sc, x1.x * sc, x1.y * sc, x1.z * sc, x1.w * sc};
-    st16_nt(dqkv + (long)r * 3L * D + c, pack8(f));
-#pragma unroll
-    for (int k = 0; k < 8; ++k) cs[k] += f[k];
-  }
-#pragma unroll
-  for (int k = 0; k < 8; ++k) red[g * D + c + k] = cs[k];
-  __syncthreads();
-  for (int col = threadIdx.x; col < D; col += blockDim.x) {
-    float s = 0.f;
-    for (int i = 0; i < rpb; ++i) s += red[i * D + col];
-    atomicAdd(dbias + col, s);
-  }
-}
-
 template <int NKS, int KW>
 constexpr int bwd_smem() {
   constexpr int NH = (NKS + 3) / 4, NO = (NKS + 1) / 2, KB = 32 * KW, TILES = 2 * NO;
@@ -940,7 +892,7 @@ void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, uint32_t* dmask, 
 
 void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse,
                    const uint32_t* dmask, float* delta, float* dq, bf16_t* dqkv, int B, int T, int H,
-                   int hd, float p, uint64_t seed, hipStream_t stream, float* dbias) {
+                   int hd, float p, uint64_t seed, hipStream_t stream, float* dbias, bool delta_ready) {
   (void)seed;
   AttnArgs a{};
   a.B = B; a.T = T; a.H = H; a.hd = hd; a.D = H * hd;
@@ -951,16 +903,18 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
   a.dq = dq; a.dqkv = dqkv; a.dmask = dmask;
   const bool persistent = bwd_persistent(T, hd);
   a.dq_part = persistent ? 0 : (long)B * T * H * hd;
-  // qkv bias gradient fused into the key-block kernel (K / V columns) and the dQ finalize (Q
-  // columns); the persistent schedule and very wide rows take the separate column-sum pass
+  // qkv bias gradient: the K / V columns fused into the key-block kernel; the Q columns by a
+  // column-sum pass over dQ after the finalize (summing them inside the finalize, a thread per
+  // 8-column chunk sweeping rows, made it 146 vs 104 + 16 us at B = 64); the persistent schedule
+  // takes the column-sum pass over all of dqkv
   const int D = H * hd;
-  const int cpb = D / 8, rpb = cpb <= 768 ? std::max(1, 768 / cpb) : 0;
-  const bool fuse_db = dbias && !persistent && rpb > 0;
+  const bool fuse_db = dbias && !persistent;
   a.dbias = fuse_db ? dbias : nullptr;
   int lg = 0;
   while ((8 << lg) < hd) ++lg;
   const long nthreads = (long)B * T * H << lg;
-  attn_bwd_pre_kernel<<<(unsigned)cdiv(nthreads, 256), 256, 0, stream>>>(dout, out, delta, B * T, T, H, hd, lg);
+  if (!delta_ready)
+    attn_bwd_pre_kernel<<<(unsigned)cdiv(nthreads, 256), 256, 0, stream>>>(dout, out, delta, B * T, T, H, hd, lg);
   switch (nks_for(hd)) {
     case 1: launch_bwd<1, 8>(a, stream); break;
     case 2: launch_bwd<2, 8>(a, stream); break;
@@ -969,16 +923,13 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
     case 6: launch_bwd<6, 4>(a, stream); break;
     default: launch_bwd<8, 4>(a, stream); break;
   }
-  if (fuse_db) {
-    const int grid = std::min(4 * num_cus(), cdiv(B * T, rpb));
-    attn_dq_finalize_bias_kernel<<<grid, cpb * rpb, rpb * D * 4, stream>>>(
-        dq, dqkv, dbias, B * T, D, T, bwd_keys_per_block(hd), a.dq_part, 0.6931471805599453f);
-  } else if (!persistent) {
+  if (!persistent) {
     const long n8 = (long)B * T * (H * hd / 8);
     attn_dq_finalize_kernel<<<(unsigned)cdiv(n8, 256), 256, 0, stream>>>(
         dq, dqkv, B * T, H * hd, T, bwd_keys_per_block(hd), a.dq_part, 0.6931471805599453f);
   }
-  if (dbias && !fuse_db) bias_grad(dqkv, dbias, (long)B * T, 3 * D, stream);
+  if (fuse_db) bias_grad(dqkv, dbias, (long)B * T, D, stream, 3L * D);  // Q columns
+  else if (dbias) bias_grad(dqkv, dbias, (long)B * T, 3 * D, stream);
 }
 
 void attention_set_bwd_mode(int mode) { g_bwd_mode = mode; }

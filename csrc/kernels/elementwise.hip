@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void dropout_bias_grad_kernel(const bf16_t* __
 // per column per block-row (RB-way, tiny).
 template <int CVB>
 __global__ __launch_bounds__(256) void bias_grad_kernel(const bf16_t* __restrict__ dy,
-                                                        float* __restrict__ db, int M, int N) {
+                                                        float* __restrict__ db, int M, int N, long ld) {
   constexpr int RG = 256 / CVB;
   __shared__ __attribute__((aligned(16))) float red[RG][CVB * 8];
   const int cv = threadIdx.x % CVB, rg = threadIdx.x / CVB;
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void bias_grad_kernel(const bf16_t* __restrict
   if (c < N) {
     for (long r = (long)blockIdx.y * RG + rg; r < M; r += (long)gridDim.y * RG) {
       float g[8];
-      unpack8(ld16(dy + r * N + c), g);
+      unpack8(ld16(dy + r * ld + c), g);
 #pragma unroll
       for (int j = 0; j < 8; ++j) s[j] += g[j];
     }
@@ -281,13 +281,14 @@ void transpose(const bf16_t* src, bf16_t* dst, int R, int C, int ldd, hipStream_
   transpose_kernel<<<dim3(cdiv(C, 128), cdiv(ldd, 128)), 256, 0, stream>>>(src, dst, R, C, ldd);
 }
 
-void bias_grad(const bf16_t* dy, float* db, long M, int N, hipStream_t stream) {
+void bias_grad(const bf16_t* dy, float* db, long M, int N, hipStream_t stream, long ld) {
   const int cvb = bias_cvb(N);
   const dim3 grid = bias_grid(M, N, cvb);
+  if (ld <= 0) ld = N;
   if (cvb == 32)
-    bias_grad_kernel<32><<<grid, 256, 0, stream>>>(dy, db, (int)M, N);
+    bias_grad_kernel<32><<<grid, 256, 0, stream>>>(dy, db, (int)M, N, ld);
   else
-    bias_grad_kernel<64><<<grid, 256, 0, stream>>>(dy, db, (int)M, N);
+    bias_grad_kernel<64><<<grid, 256, 0, stream>>>(dy, db, (int)M, N, ld);
 }
 
 }  // namespace mg

@@ -80,6 +80,9 @@ struct GemmArgs {
   uint32_t a_bytes, b_bytes;  // buffer-resource extents (out-of-range reads return 0)
   unsigned long long* dbg;    // MG_GEMM_STAMPS diagnostic builds only: per-wave phase timestamps
   float* dbias;               // EPI 4: += column sums of the output (the bias gradient), or null
+  float* delta;               // EPI 5: attention delta[(b H + h) T + t] = sum_d C[m, h hd + d] aux[m, ..]
+  int dT, dH, dhd;            // EPI 5: sequence length, heads, head dim (hd in {8, 16, 32, 64})
+  long drow0;                 // EPI 5: global row of this launch's row 0 (row-chunked launches)
   int nt_out;                 // non-temporal bf16 output stores (see gemm() below)
 };
 
@@ -269,12 +272,25 @@ MG_DEVICE void staged_rows(const GemmArgs& args, const char* st, const uint4 (&s
       const float4 b = *reinterpret_cast<const float4*>(row + p * 32 + 16);
       float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
       const uint32_t w[4] = {sd[it].x, sd[it].y, sd[it].z, sd[it].w};
+      float dot = 0.f;  // EPI 5: this piece's share of sum_d dO * O
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float s = bf2f((w[k >> 1] >> (16 * (k & 1))) & 0xffffu);
-        v[k] = EPI == 3 ? v[k] + s : v[k] * s;
+        if constexpr (EPI == 5) dot = __builtin_fmaf(v[k], s, dot);
+        else v[k] = EPI == 3 ? v[k] + s : v[k] * s;
       }
       y = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+      if constexpr (EPI == 5) {
+        // the hd / 8 consecutive lanes of a (row, head) -- aligned inside the row's PR lanes,
+        // since the wave-tile width is a multiple of hd -- fold, the first one stores
+        const int g8 = args.dhd >> 3;
+        for (int o = 1; o < g8; o <<= 1) dot += __shfl_xor(dot, o, 64);
+        if ((p & (g8 - 1)) == 0 && (!CHECK || m < args.M)) {
+          const long gm = args.drow0 + m;
+          const int bb = (int)(gm / args.dT), t = (int)(gm % args.dT);
+          args.delta[((long)bb * args.dH + n / args.dhd) * args.dT + t] = dot;
+        }
+      }
       if constexpr (EPI == 4 && staged_dbias<CF>()) {  // column sums (fp32, before the bf16 rounding)
         if constexpr (CHECK) {
           const bool ok = m < args.M;
@@ -314,7 +330,7 @@ MG_DEVICE void staged_rows(const GemmArgs& args, const char* st, const uint4 (&s
 template <class CF, int EPI, int LDSW>
 MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int m0, int n0,
                                int wm, int wn, int wid, int lane, char* smem) {
-  constexpr bool F32 = EPI == 3 || EPI == 4;     // staged before a bf16 side input is applied
+  constexpr bool F32 = EPI == 3 || EPI == 4 || EPI == 5;  // staged before a bf16 side input is applied
   constexpr int PL = EPI == 2 ? 2 : 1;           // planes: y (+ GELU' for EPI 2)
   constexpr int S = CF::WTN * (F32 ? 4 : 2) + 16;  // row stride: rows 4 banks apart (b64/b128 writes)
   constexpr int CHF = stage_chf(CF::FM, 16 * S * PL, LDSW);  // fragment rows per pass
@@ -1225,9 +1241,11 @@ int gemm_get_variant() { return g_variant; }
 void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long lda, long ldb,
           long ldc, int M, int N, int K, int a_ext, int b_ext, int ka, int kb, const bf16_t* bias,
           bf16_t* aux, const bf16_t* resid, float p, uint64_t seed, hipStream_t stream,
-          size_t a_bytes, size_t b_bytes, float* dbias) {
+          size_t a_bytes, size_t b_bytes, float* dbias, const GemmDelta* dl) {
   GemmArgs a;
   a.dbias = dbias;
+  a.delta = dl ? dl->delta : nullptr;
+  a.dT = dl ? dl->T : 1; a.dH = dl ? dl->H : 1; a.dhd = dl ? dl->hd : 8; a.drow0 = dl ? dl->row0 : 0;
   a.a_bytes = (uint32_t)std::min<size_t>(a_bytes, 0xFFFFFF00u);
   a.b_bytes = (uint32_t)std::min<size_t>(b_bytes, 0xFFFFFF00u);
   a.A = A; a.B = B; a.C = C; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
@@ -1255,6 +1273,7 @@ void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long l
     else dispatch<true, true, 4, false>(a, stream);  // dgrad as NT against a transposed weight
   } else if (layout == 1) {
     if (epi == 4) dispatch<true, false, 4, false>(a, stream);
+    else if (epi == 5) dispatch<true, false, 5, false>(a, stream);
     else dispatch<true, false, 0, false>(a, stream);
   } else {
     dispatch<false, false, 0, true>(a, stream);

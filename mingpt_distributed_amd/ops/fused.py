@@ -60,6 +60,12 @@ _FC_DBIAS_FUSED = os.environ.get("MINGPT_FC_DBIAS_FUSED", "1") == "1"
 # registers, dQ columns in the dQ finalize) instead of a separate 300 MB pass over dqkv.
 # MINGPT_QKV_DBIAS_FUSED=0 restores the separate bias_grad kernel.
 _QKV_DBIAS_FUSED = os.environ.get("MINGPT_QKV_DBIAS_FUSED", "1") == "1"
+# MINGPT_DELTA_FUSED=1: the attention backward's delta = rowsum(dO * O) computed in the epilogue of
+# the GEMM that produces dO (gemm.hip epilogue 5) instead of attn_bwd_pre_kernel.  Off by default:
+# the K = 768 projection GEMM pays more for the fp32 staging and the O loads in its epilogue (282 vs
+# ~160 us at B = 128) than the separate 73 us pass costs (one-box A/B 1,006.0k / 995.0k fused vs
+# 1,007.7k / 998.8k, profiles/round2_s10_delta_epilogue_ab.txt).
+_DELTA_FUSED = os.environ.get("MINGPT_DELTA_FUSED", "0") == "1"
 
 
 # Library calls cost more host time per launch than the extension's; small models (gpt-mini:
@@ -183,12 +189,20 @@ class TransformerBlockFn(_EngineFn):
             dz = dx1
             C.bias_grad(dz, g[id(bo)][0])
         _wgrad(dz, y, g[id(wo)][0])
-        dy = _dgrad(dz, wo)
+        hd = wo.shape[0] // H
+        delta = None
+        if _DELTA_FUSED and hd in (8, 16, 32, 64) and not (_DGRAD_BLAS and _big(dz.shape[0], wo.shape[1], wo.shape[0])):
+            # the attention backward's rowsum(dO * O) in the dO GEMM's epilogue (no separate pass)
+            delta = torch.empty(B * H * T, dtype=torch.float32, device=dz.device)
+            dy = G.gemm_nn(dz, wo, epi="delta", aux=y, delta=(delta, T, H, hd))
+        else:
+            dy = _dgrad(dz, wo)
         if _QKV_DBIAS_FUSED:  # qkv bias gradient summed inside the attention backward
             dqkv = C.attention_bwd(qkv, y, dy, lse, amask, B, T, H, float(p_attn), ctx.seeds[0],
-                                   g[id(bqkv)][0])
+                                   g[id(bqkv)][0], delta)
         else:
-            dqkv = C.attention_bwd(qkv, y, dy, lse, amask, B, T, H, float(p_attn), ctx.seeds[0])
+            dqkv = C.attention_bwd(qkv, y, dy, lse, amask, B, T, H, float(p_attn), ctx.seeds[0],
+                                   None, delta)
             C.bias_grad(dqkv, g[id(bqkv)][0])
         _wgrad(dqkv, h, g[id(wqkv)][0])
         dh = _dgrad(dqkv, wqkv)

@@ -22,7 +22,7 @@ import torch
 
 from ._ext import ext
 
-EPI_NONE, EPI_BIAS, EPI_GELU, EPI_RESID, EPI_GELU_BWD = 0, 1, 2, 3, 4
+EPI_NONE, EPI_BIAS, EPI_GELU, EPI_RESID, EPI_GELU_BWD, EPI_DELTA = 0, 1, 2, 3, 4, 5
 
 
 _MAX_BYTES = 0xFFFFFF00  # the kernels address each operand through a 32-bit buffer descriptor
@@ -97,21 +97,32 @@ def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, *, epi: str = "none",
 
 
 def gemm_nn(a: torch.Tensor, b: torch.Tensor, *, epi: str = "none",
-            aux: Optional[torch.Tensor] = None, dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
+            aux: Optional[torch.Tensor] = None, dbias: Optional[torch.Tensor] = None,
+            delta: Optional[tuple] = None) -> torch.Tensor:
     """C = A @ B (B row-major [K, N]); ``gelu_bwd`` multiplies by ``aux`` (a stored GELU') and,
-    with ``dbias`` (fp32 [N]), adds the column sums of the stored C into it (staged epilogue)."""
+    with ``dbias`` (fp32 [N]), adds the column sums of the stored C into it (staged epilogue).
+    ``delta`` epilogue (``delta=(out, T, H, hd)``, hd in {8, 16, 32, 64}): C is the attention
+    output's gradient dO and ``aux`` the attention output O; writes the attention backward's
+    out[(b H + h) T + t] = sum_d dO * O per head (fp32 products of the unrounded dO)."""
     _check2d(a, "A")
     _check2d(b, "B")
     M, K = a.shape
     N = b.shape[1]
     c = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
-    code = {"none": EPI_NONE, "gelu_bwd": EPI_GELU_BWD}[epi]
+    code = {"none": EPI_NONE, "gelu_bwd": EPI_GELU_BWD, "delta": EPI_DELTA}[epi]
     if dbias is not None and code != EPI_GELU_BWD:
         raise ValueError("gemm_nn: dbias is fused only into the gelu_bwd epilogue")
+    if (code == EPI_DELTA) != (delta is not None):
+        raise ValueError("gemm_nn: the delta epilogue takes delta=(out, T, H, hd)")
+    dkw = {}
+    if delta is not None:
+        out, T, H, hd = delta
+        dkw = dict(delta=out, dT=int(T), dH=int(H), dhd=int(hd))
     chunks = _row_chunks(M, 2 * K, 2 * N)
     for r0, r1 in chunks:
         sl = (lambda t: t if t is None or len(chunks) == 1 else t[r0:r1])
-        ext().gemm(sl(a), b, sl(c), 1, code, None, sl(aux), None, 0.0, 0, r1 - r0, N, dbias)
+        ext().gemm(sl(a), b, sl(c), 1, code, None, sl(aux), None, 0.0, 0, r1 - r0, N, dbias,
+                   **(dict(dkw, row0=r0) if dkw else {}))
     return c
 
 

@@ -162,3 +162,19 @@ def test_row_chunked_launches_match(monkeypatch):
     torch.testing.assert_close(G.gemm_nn(dy, w), ref_nn, atol=0, rtol=0)
     torch.testing.assert_close(G.gemm_tn_acc(dy, a, torch.zeros(N, K, device="cuda")), ref_tn,
                                atol=1e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("M,T,hd", [(1000, 250, 64), (8192, 1024, 64), (4096, 512, 32), (2048, 256, 16)])
+def test_dgrad_delta_epilogue(M, T, hd):
+    """Epilogue 5: the dO GEMM (dO = dZ Wo) also writes the attention backward's
+    delta[(b H + h) T + t] = sum_d dO * O per head (O = aux); T128 (partial tiles) and W4 shapes."""
+    D = 768
+    H = D // hd
+    dz, wo, y = _bf(M, D, seed=31), _bf(D, D, seed=32, scale=0.05), _bf(M, D, seed=33)
+    delta = torch.full((M // T * H * T,), float("nan"), device=DEV)
+    dy = G.gemm_nn(dz, wo, epi="delta", aux=y, delta=(delta, T, H, hd))
+    ref = dz.float() @ wo.float()
+    _check(dy, ref, D)
+    dref = (ref * y.float()).view(M // T, T, H, hd).sum(-1).permute(0, 2, 1).reshape(-1)
+    torch.testing.assert_close(delta, dref, atol=2e-2, rtol=1e-2)
+    torch.testing.assert_close(dy, G.gemm_nn(dz, wo), atol=0, rtol=0)  # the stored dO is unchanged
