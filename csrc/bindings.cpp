@@ -387,8 +387,8 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     TORCH_CHECK(resid->numel() == c.numel() && ldc == N, "gemm: resid shape");
     res_p = bp(*resid);
   }
-  TORCH_CHECK((size_t)a.numel() * 2 < 0xFFFFFF00u && (size_t)b.numel() * 2 < 0xFFFFFF00u,
-              "gemm: operands must be < 4 GiB (32-bit buffer offsets)");
+  // operands past 4 GiB are fine: every block's buffer descriptor starts at its own tile / split
+  // origin (gemm.hip Stager::retarget; split-K ranges are capped below 4 GiB by set_split)
   float* dbias_p = nullptr;
   if (dbias.has_value() && dbias->defined()) {
     CHECK_F32(*dbias);

@@ -77,7 +77,7 @@ struct GemmArgs {
   float scale;
   int tiles_m, tiles_n;
   int splits, kchunk;         // split-K (fp32-accumulate layout only): K range per split
-  uint32_t a_bytes, b_bytes;  // buffer-resource extents (out-of-range reads return 0)
+  uint64_t a_bytes, b_bytes;  // operand sizes; each block's descriptor spans <= 4 GiB from its origin
   unsigned long long* dbg;    // MG_GEMM_STAMPS diagnostic builds only: per-wave phase timestamps
   float* dbias;               // EPI 4: += column sums of the output (the bias gradient), or null
   float* delta;               // EPI 5: attention delta[(b H + h) T + t] = sum_d C[m, h hd + d] aux[m, ..]
@@ -113,7 +113,8 @@ struct Stager {
   uint32_t voff[PER];
   const char* ptr;  // operand base
   const char* base;
-  uint32_t total, bytes, step;
+  uint64_t total;  // operand bytes (may exceed 4 GiB: the descriptor starts at the tile / split origin)
+  uint32_t bytes, step;
   long ld;
   int kbeg, klim, tail_t, swid;
 
@@ -121,7 +122,7 @@ struct Stager {
   // in the descriptor base, see retarget), so they are the same for every tile; rows past the
   // operand read as zero through the descriptor extent (the operand buffer ends at its last row).
   // m/n-contiguous operands: absolute offsets with a per-lane column check.
-  MG_DEVICE void init(const bf16_t* p, uint32_t tot, long ld_, int r0, int ext, int kbeg_, int kvalid,
+  MG_DEVICE void init(const bf16_t* p, uint64_t tot, long ld_, int r0, int ext, int kbeg_, int kvalid,
                       int kend, int wid, int lane) {
     ptr = reinterpret_cast<const char*>(p);
     total = tot;
@@ -150,7 +151,8 @@ struct Stager {
   MG_DEVICE void retarget(int r0) {
     const uint64_t o = KC ? (uint64_t)((long)r0 * ld + kbeg) * 2 : (uint64_t)kbeg * ld * 2;
     base = ptr + o;
-    bytes = total > o ? total - (uint32_t)o : 0u;
+    const uint64_t rest = total > o ? total - o : 0u;  // a block never reaches 4 GiB past its origin
+    bytes = rest < 0xFFFFFF00u ? (uint32_t)rest : 0xFFFFFF00u;
   }
   // piece-level form for hand-interleaved schedules: descriptor once per tile, then piece(i)
   MG_DEVICE __amdgpu_buffer_rsrc_t rsrc(int t) const { return tile_rsrc(base, bytes, step, t); }
@@ -777,12 +779,14 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const GemmArgs args) {
   const uint32_t sta = AK ? BK * 2 : (uint32_t)(BK * args.lda * 2);
   const uint32_t stb = BKC ? BK * 2 : (uint32_t)(BK * args.ldb * 2);
   // operand bases at the split's first k; extents from there
-  const uint32_t a_k0 = AK ? (uint32_t)kbeg * 2 : (uint32_t)((long)kbeg * args.lda * 2);
-  const uint32_t b_k0 = BKC ? (uint32_t)kbeg * 2 : (uint32_t)((long)kbeg * args.ldb * 2);
+  // k-contiguous operands carry the tile's row origin in the base (not in the 32-bit per-lane
+  // offsets), so operands past 4 GiB address correctly
+  const uint64_t a_k0 = AK ? ((uint64_t)m0 * args.lda + kbeg) * 2 : (uint64_t)kbeg * args.lda * 2;
+  const uint64_t b_k0 = BKC ? ((uint64_t)n0 * args.ldb + kbeg) * 2 : (uint64_t)kbeg * args.ldb * 2;
   const char* abase = reinterpret_cast<const char*>(args.A) + a_k0;
   const char* bbase = reinterpret_cast<const char*>(args.B) + b_k0;
-  const uint32_t abytes = args.a_bytes > a_k0 ? args.a_bytes - a_k0 : 0u;
-  const uint32_t bbytes = args.b_bytes > b_k0 ? args.b_bytes - b_k0 : 0u;
+  const uint32_t abytes = (uint32_t)min<uint64_t>(args.a_bytes > a_k0 ? args.a_bytes - a_k0 : 0u, 0xFFFFFF00u);
+  const uint32_t bbytes = (uint32_t)min<uint64_t>(args.b_bytes > b_k0 ? args.b_bytes - b_k0 : 0u, 0xFFFFFF00u);
   // k limit relative to the split start (ka/kb: reads as zero beyond), and the partial tile
   const int kla = min(args.ka, kbeg + args.kchunk) - kbeg, klb = min(args.kb, kbeg + args.kchunk) - kbeg;
   const int tail_t = min(kla, klb) / BK;  // first K-tile needing per-lane k checks (usually none)
@@ -791,8 +795,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const GemmArgs args) {
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh) {
-      pa[h][kh] = ppk::make_piece<AK>(args.lda, m0, args.a_ext, h, kh, wid, lane);
-      pb[h][kh] = ppk::make_piece<BKC>(args.ldb, n0, args.b_ext, h, kh, wid, lane);
+      pa[h][kh] = ppk::make_piece<AK>(args.lda, AK ? 0 : m0, AK ? args.a_ext - m0 : args.a_ext, h, kh, wid, lane);
+      pb[h][kh] = ppk::make_piece<BKC>(args.ldb, BKC ? 0 : n0, BKC ? args.b_ext - n0 : args.b_ext, h, kh, wid, lane);
     }
   auto dst_of = [&](int t, int opoff, int ro, int slot) -> char* {
     return t < nk ? smem + (t & 1) * ppk::BUF + opoff + ro + swid * 1024
@@ -898,11 +902,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const GemmArgs args) {
 // rounds x per-block work, where rounds = ceil(blocks / concurrent slots) and per-block work =
 // its K-tiles + ~2 tiles of prologue/epilogue (the atomic write-back).  A naive "fill the chip"
 // split leaves a mostly idle second round (e.g. 144 tiles x 4 = 576 blocks on 512 slots).
-static int choose_split(int tiles, int slots, int nkt, int ovh) {
-  int best = 1;
+static int choose_split(int tiles, int slots, int nkt, int ovh, int spmin = 1) {
+  int best = spmin;
   long bc = -1;
-  const int maxsp = std::max(1, std::min(32, nkt / 4));
-  for (int sp = 1; sp <= maxsp; ++sp) {
+  const int maxsp = std::max(spmin, std::min(32, nkt / 4));
+  for (int sp = spmin; sp <= maxsp; ++sp) {
     const long rounds = ((long)tiles * sp + slots - 1) / slots;
     const long c = rounds * (cdiv(nkt, sp) + ovh);
     if (bc < 0 || c * 20 < bc * 19) {  // a further split must save >= 5%
@@ -916,7 +920,14 @@ static int choose_split(int tiles, int slots, int nkt, int ovh) {
 // ovh: per-block prologue + atomic write-back in K-tile units (grows with the tile area)
 static void set_split(GemmArgs& a, int slots, int ovh) {
   const int nkt = cdiv(a.K, BK);
-  const int sp = choose_split(a.tiles_m * a.tiles_n, slots, nkt, ovh);
+  // a split's K range of an m/n-contiguous operand (k rows of ld elements) must stay inside one
+  // buffer descriptor (< 4 GiB from the split's origin): the LM head's weight gradient at 131k
+  // tokens reads 13 GB of logits gradients in one launch (6 splits: half the fp32 atomic bytes of
+  // the four row-chunked launches of 3 splits each, and no per-launch round quantisation)
+  const uint64_t row_bytes = (uint64_t)std::max(a.lda, a.ldb) * 2;
+  int spmin = 1;
+  while (spmin < nkt && (uint64_t)cdiv(nkt, spmin) * BK * row_bytes >= 0xF0000000ull) ++spmin;
+  const int sp = choose_split(a.tiles_m * a.tiles_n, slots, nkt, ovh, spmin);
   a.kchunk = cdiv(nkt, sp) * BK;
   a.splits = cdiv(a.K, a.kchunk);
 }
@@ -1246,8 +1257,8 @@ void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long l
   a.dbias = dbias;
   a.delta = dl ? dl->delta : nullptr;
   a.dT = dl ? dl->T : 1; a.dH = dl ? dl->H : 1; a.dhd = dl ? dl->hd : 8; a.drow0 = dl ? dl->row0 : 0;
-  a.a_bytes = (uint32_t)std::min<size_t>(a_bytes, 0xFFFFFF00u);
-  a.b_bytes = (uint32_t)std::min<size_t>(b_bytes, 0xFFFFFF00u);
+  a.a_bytes = a_bytes;  // full sizes: each block's descriptor starts at its own tile / split origin
+  a.b_bytes = b_bytes;
   a.A = A; a.B = B; a.C = C; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.M = M; a.N = N; a.K = K; a.a_ext = a_ext; a.b_ext = b_ext; a.ka = ka; a.kb = kb;
   a.bias = bias; a.aux = aux; a.resid = resid; a.seed = seed; a.sofs = graph_seed_ofs();

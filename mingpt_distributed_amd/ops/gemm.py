@@ -25,15 +25,18 @@ from ._ext import ext
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_RESID, EPI_GELU_BWD, EPI_DELTA = 0, 1, 2, 3, 4, 5
 
 
-_MAX_BYTES = 0xFFFFFF00  # the kernels address each operand through a 32-bit buffer descriptor
+# Row-chunked launches are no longer needed for operands past 4 GiB (the GPT-2 logits beyond ~42k
+# tokens): each block's buffer descriptor starts at its own tile / split origin and split-K ranges
+# stay below 4 GiB (gemm.hip set_split).  The mechanism stays for tests (monkeypatch this cap).
+_MAX_BYTES = 1 << 62
 # data gradients NN from the stored weight (MINGPT_DGRAD_NN=0: NT against a transposed copy)
 _DGRAD_NN = os.environ.get("MINGPT_DGRAD_NN", "1") == "1"
 
 
 def _row_chunks(M: int, *row_bytes: int):
     """Row ranges [r0, r1) of an M-row operand such that no chunk of any operand whose rows are
-    ``row_bytes`` wide reaches 4 GiB (e.g. GPT-2 logits at > 42k tokens per GPU): the M-chunked
-    launches are exact (the epilogues used here do not depend on the global row index)."""
+    ``row_bytes`` wide reaches ``_MAX_BYTES``: the M-chunked launches are exact (the epilogues used
+    here do not depend on the global row index, the delta epilogue takes its row offset)."""
     cap = max(256, (_MAX_BYTES // max(max(row_bytes), 1)) // 256 * 256)
     if M <= cap:
         return [(0, M)]

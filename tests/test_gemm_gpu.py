@@ -178,3 +178,28 @@ def test_dgrad_delta_epilogue(M, T, hd):
     dref = (ref * y.float()).view(M // T, T, H, hd).sum(-1).permute(0, 2, 1).reshape(-1)
     torch.testing.assert_close(delta, dref, atol=2e-2, rtol=1e-2)
     torch.testing.assert_close(dy, G.gemm_nn(dz, wo), atol=0, rtol=0)  # the stored dO is unchanged
+
+
+def test_operands_past_4gib_single_launch(monkeypatch):
+    """Operands past 4 GiB (the GPT-2 logits and their gradient beyond ~42k tokens) run as ONE
+    launch: every block's buffer descriptor starts at its own tile / split origin, split-K ranges
+    stay below 4 GiB.  Equal to the row-chunked launches (each operand chunk < 4 GiB)."""
+    torch.manual_seed(0)
+    M, V, D = 43008, 50304, 768  # [M, V] bf16 = 4.33 GB
+    h = (torch.randn(M, D, device=DEV) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(V, D, device=DEV) * 0.05).to(torch.bfloat16)
+    logits = G.gemm_nt(h, w, ld=V)
+    dl = (torch.randn(M, V, device=DEV) * 0.01).to(torch.bfloat16)
+    dh = G.gemm_dgrad(dl, w)
+    gw = torch.zeros(V, D, device=DEV)
+    G.gemm_tn_acc(dl, h, gw)
+    monkeypatch.setattr(G, "_MAX_BYTES", 0x7FFFFFFF)  # chunks of < 2 GiB rows: the old launches
+    assert len(G._row_chunks(M, 2 * V)) > 1
+    torch.testing.assert_close(logits, G.gemm_nt(h, w, ld=V), atol=0, rtol=0)
+    torch.testing.assert_close(dh, G.gemm_dgrad(dl, w), atol=0, rtol=0)
+    gw2 = torch.zeros(V, D, device=DEV)
+    G.gemm_tn_acc(dl, h, gw2)
+    torch.testing.assert_close(gw, gw2, atol=1e-3 * gw2.abs().max().item(), rtol=1e-3)  # split order
+    # and the rows past 4 GiB really are read: the last 512 rows' logits against fp32 torch
+    ref = h[-512:].float() @ w.float().t()
+    torch.testing.assert_close(logits[-512:].float(), ref, atol=2e-2, rtol=2e-2)
