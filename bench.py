@@ -15,7 +15,16 @@ reference's dropout (0.1) active.
 reporting a smaller run under the requested GPU count.
 
 W untimed warmup steps, then K steps bracketed by barrier + device sync; the max over ranks is
-reported.  ``vs_baseline`` divides by N x the measured single-GPU torch-eager self-baseline of the
+reported.  The same engine is then timed again at ``--also-batch`` sequences per GPU (default 64,
+the reference's per-GPU batch, ``/root/reference/mingpt/gpt2_config.yaml:14``), reported under
+``extra`` so that rounds stay comparable at a fixed config.
+
+Diagnostics in the JSON line (``comm``): the RCCL version the ranks loaded, every rank's device
+name and PCI bus id, the bucket plan (count, bytes per bucket in the wire dtype), and
+``comm_exposed_ms`` -- the mean device time per timed step from the end of backward's last
+kernel to the end of the gradient communication (``StepEngine.comm_exposed_ms``): the
+communication NOT hidden under backward.  ``--comm-at-world1`` runs the RCCL path on a one-rank
+group at N = 1 as a plumbing check of those fields.  ``vs_baseline`` divides by N x the measured single-GPU torch-eager self-baseline of the
 same step at the same per-GPU batch, i.e. the per-GPU speedup over stock
 PyTorch-ROCm (the reference publishes no numbers).
 """
@@ -58,6 +67,33 @@ def _launch_ranks(n: int) -> int:
     return subprocess.call(cmd)
 
 
+def _comm_diag(eng, info, N, comm_ms):
+    """Self-diagnosis of the data-parallel path (collective: every rank calls it)."""
+    import torch.distributed as dist
+
+    try:
+        v = torch.cuda.nccl.version()
+        rccl = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:  # noqa: BLE001 - diagnostics only
+        rccl = None
+    props = torch.cuda.get_device_properties(info.device)
+    bus = "%04x:%02x:%02x" % (getattr(props, "pci_domain_id", 0), getattr(props, "pci_bus_id", 0),
+                              getattr(props, "pci_device_id", 0))
+    me = {"rank": info.rank, "local_rank": info.local_rank, "device": torch.cuda.get_device_name(info.device),
+          "pci_bus_id": bus, "hostname": socket.gethostname()}
+    ranks = [me]
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        ranks = [None] * dist.get_world_size()
+        dist.all_gather_object(ranks, me)
+    out = {"rccl_version": rccl, "world_size": N, "backend": info.backend, "ranks": ranks,
+           "comm_exposed_ms": None if comm_ms is None else round(comm_ms, 3)}
+    if eng.dp is not None:
+        out.update(eng.dp.comm_plan())
+    else:
+        out.update({"n_buckets": None, "bucket_bytes": None, "wire_dtype": None, "collective": None})
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -79,6 +115,10 @@ def main():
     ap.add_argument("--profile", default="", help="write a torch.profiler trace to this dir")
     ap.add_argument("--graph", action="store_true",
                     help="replay each step as one hipGraph (single GPU; StepEngine.graph_step)")
+    ap.add_argument("--also-batch", type=int, default=64,
+                    help="second timed pass at this per-GPU batch (0: skip), reported under 'extra'")
+    ap.add_argument("--comm-at-world1", action="store_true",
+                    help="N = 1: drive the RCCL collective path on a one-rank group (plumbing check)")
     a = ap.parse_args()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_launch_ranks(a.gpus))  # parent: no GPU call happens in this process
@@ -87,7 +127,7 @@ def main():
     from mingpt_distributed_amd.parallel import dist as D
     from mingpt_distributed_amd.trainer import StepEngine
 
-    info = D.init_distributed(device="cuda")
+    info = D.init_distributed(device="cuda", group_at_world1=a.comm_at_world1)
     N = D.world_size()  # from the process group itself, not the env
     if N != a.gpus:
         print(f"bench.py: --gpus {a.gpus} but the process group has {N} rank(s); refusing to "
@@ -102,38 +142,61 @@ def main():
     model = GPT(cfg, verbose=info.rank == 0)
     eng = StepEngine(model, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, grad_clip=1.0,
                      bucket_mb=a.bucket_mb, zero1=a.zero1,
-                     reduce_dtype=torch.bfloat16 if a.reduce_dtype == "bf16" else None)
+                     reduce_dtype=torch.bfloat16 if a.reduce_dtype == "bf16" else None,
+                     comm_at_world1=a.comm_at_world1)
     g = torch.Generator(device=eng.device).manual_seed(99 + info.rank)
-    nb = 4
-    xs = [torch.randint(0, a.vocab, (a.batch, a.seq), device=eng.device, generator=g) for _ in range(nb)]
-    ys = [torch.randint(0, a.vocab, (a.batch, a.seq), device=eng.device, generator=g) for _ in range(nb)]
-
     step = (lambda x, y: eng.graph_step(x, y)) if a.graph else (lambda x, y: eng.train_step([(x, y)]))
-    for i in range(a.warmup):
-        loss = step(xs[i % nb], ys[i % nb])
-    D.barrier()
-    torch.cuda.synchronize()
-    prof = None
-    if a.profile and info.rank == 0:
-        prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
-                                                  torch.profiler.ProfilerActivity.CUDA])
-        prof.__enter__()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        loss = step(xs[i % nb], ys[i % nb])
-    torch.cuda.synchronize()
-    D.barrier()
-    dt = time.perf_counter() - t0
-    if prof is not None:
-        prof.__exit__(None, None, None)
-        os.makedirs(a.profile, exist_ok=True)
-        prof.export_chrome_trace(os.path.join(a.profile, "trace.json"))
-        with open(os.path.join(a.profile, "summary.txt"), "w") as f:
-            f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
-    dt = D.all_reduce_max(dt, eng.device)
+
+    def timed(batch, steps, warmup, profile=""):
+        """W untimed steps, then `steps` timed ones between barrier + device syncs; returns
+        (max seconds over ranks, last loss, mean exposed-comm ms or None)."""
+        nb = 4
+        xs = [torch.randint(0, a.vocab, (batch, a.seq), device=eng.device, generator=g) for _ in range(nb)]
+        ys = [torch.randint(0, a.vocab, (batch, a.seq), device=eng.device, generator=g) for _ in range(nb)]
+        for i in range(warmup):
+            loss = step(xs[i % nb], ys[i % nb])
+        D.barrier()
+        torch.cuda.synchronize()
+        eng.measure_comm = eng.dp is not None and not a.graph
+        eng.comm_exposed_ms()  # drop warm-up events
+        prof = None
+        if profile and info.rank == 0:
+            prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
+                                                      torch.profiler.ProfilerActivity.CUDA])
+            prof.__enter__()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            loss = step(xs[i % nb], ys[i % nb])
+        torch.cuda.synchronize()
+        D.barrier()
+        dt = time.perf_counter() - t0
+        eng.measure_comm = False
+        if prof is not None:
+            prof.__exit__(None, None, None)
+            os.makedirs(profile, exist_ok=True)
+            prof.export_chrome_trace(os.path.join(profile, "trace.json"))
+            with open(os.path.join(profile, "summary.txt"), "w") as f:
+                f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+        comm = eng.comm_exposed_ms()
+        if comm is not None:
+            comm = D.all_reduce_max(comm, eng.device)
+        return D.all_reduce_max(dt, eng.device), loss, comm
+
+    dt, loss, comm_ms = timed(a.batch, a.steps, a.warmup, a.profile)
     loss_v = D.all_reduce_mean(loss.float()).item()
     tokens = a.batch * a.seq * a.steps * N
     value = tokens / dt
+    max_mem = torch.cuda.max_memory_allocated() / 2 ** 30
+    extra = {}
+    if a.also_batch and a.also_batch != a.batch:
+        dt2, _, comm2 = timed(a.also_batch, a.steps, min(a.warmup, 2))
+        v2 = a.also_batch * a.seq * a.steps * N / dt2
+        base2 = BASELINE_TOK_S_PER_GPU.get(a.also_batch)
+        extra[f"batch{a.also_batch}"] = {
+            "value": round(v2, 1), "ms_per_step": round(dt2 / a.steps * 1e3, 3),
+            "global_batch": a.also_batch * N, "comm_exposed_ms": None if comm2 is None else round(comm2, 3),
+            "vs_baseline": round(v2 / (base2 * N), 3) if base2 and a.model == "gpt2" and a.seq == 1024 else None}
+    diag = _comm_diag(eng, info, N, comm_ms)
     if info.rank == 0:
         out = {
             "metric": "tokens/sec (whole node), GPT-2 124M seq1024 bf16" if a.model == "gpt2"
@@ -156,7 +219,9 @@ def main():
                        "bucket_mb": a.bucket_mb, "grad_reduce_dtype": a.reduce_dtype if N > 1 else None,
                        "hip_graph": bool(a.graph and N == 1)},
             "loss": round(loss_v, 4),
-            "max_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2),
+            "max_mem_gb": round(max_mem, 2),
+            "extra": extra,
+            "comm": diag,
         }
         print(json.dumps(out), flush=True)
     D.destroy()

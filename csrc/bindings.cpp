@@ -200,15 +200,21 @@ void grad_sumsq(const at::Tensor& grad, double grad_scale, const at::Tensor& out
   mg::grad_sumsq(fp(grad), grad.numel(), (float)grad_scale, fp(ws), fp(out), cur_stream());
 }
 
-// The chunk tables are built (and range-checked against these buffers) by optim.py at
-// construction; here: dtypes, sizes and the table lengths.
+// The chunk tables are built and range-checked on the host by optim.make_chunk_table, which
+// also returns the bounds it checked against (table_end: one past the last flat element any
+// chunk touches; moment_end: the same for the packed moments).  The kernels index through the
+// tables unchecked, so every buffer handed in here must cover those bounds: a table built for
+// another store (e.g. before a re-layout) fails here instead of reading or writing out of bounds.
 void grad_sumsq_chunks(const at::Tensor& chunk_start, const at::Tensor& chunk_len,
-                       const at::Tensor& grad, double grad_scale, const at::Tensor& out) {
+                       const at::Tensor& grad, double grad_scale, const at::Tensor& out,
+                       int64_t table_end) {
   CHECK_I64(chunk_start); CHECK_DEV(chunk_len); CHECK_CONTIG(grad); CHECK_F32(out);
   TORCH_CHECK(chunk_len.scalar_type() == at::kInt, "chunk_len must be int32");
   TORCH_CHECK(grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16,
               "grad must be fp32 or bf16");
   TORCH_CHECK(chunk_start.numel() == chunk_len.numel() && out.numel() >= 2);
+  TORCH_CHECK(table_end >= 0 && grad.numel() >= table_end, "grad_sumsq_chunks: chunk table reaches element ",
+              table_end, " of a ", grad.numel(), "-element gradient buffer");
   const int64_t nc = chunk_len.numel();
   if (nc == 0) { out.zero_(); return; }
   DevGuard g(grad.device());
@@ -222,7 +228,8 @@ void adamw_step(const at::Tensor& chunk_start, const at::Tensor& chunk_len,
                 const at::Tensor& chunk_wd, const c10::optional<at::Tensor>& moment_start,
                 const at::Tensor& master, const at::Tensor& param, const at::Tensor& grad,
                 const at::Tensor& m, const at::Tensor& v, const at::Tensor& norm, double lr,
-                double b1, double b2, double eps, int64_t step, double grad_scale, double clip) {
+                double b1, double b2, double eps, int64_t step, double grad_scale, double clip,
+                int64_t table_end, int64_t moment_end) {
   CHECK_I64(chunk_start); CHECK_DEV(chunk_len); CHECK_F32(chunk_wd);
   TORCH_CHECK(chunk_len.scalar_type() == at::kInt, "chunk_len must be int32");
   CHECK_F32(master); CHECK_BF16(param); CHECK_F32(m); CHECK_F32(v); CHECK_F32(norm);
@@ -231,6 +238,10 @@ void adamw_step(const at::Tensor& chunk_start, const at::Tensor& chunk_len,
               "grad must be fp32 or bf16");
   const int64_t n = master.numel();
   TORCH_CHECK(param.numel() == n && grad.numel() == n, "adamw: flat buffer size mismatch");
+  TORCH_CHECK(table_end >= 0 && n >= table_end, "adamw: chunk table reaches element ", table_end,
+              " of ", n, "-element flat buffers");
+  TORCH_CHECK(moment_end >= 0 && m.numel() >= moment_end && v.numel() >= moment_end,
+              "adamw: chunk table reaches moment ", moment_end, " of ", m.numel());
   const int64_t* ms = nullptr;
   if (moment_start.has_value() && moment_start->defined()) {
     CHECK_I64(*moment_start);
@@ -516,8 +527,12 @@ at::Tensor gemv(const at::Tensor& x, const at::Tensor& W, int64_t epi, const c10
 }
 
 // pos_dev (int32 [1] on the device, optional): the position is read by the kernel (hipGraph decode)
+// part / counters (optional): the decode state's own workspace (kernels.h); without them a
+// temporary pair is allocated for this call (tests; not for captured graphs)
 at::Tensor attention_decode(const at::Tensor& qkv_new, const at::Tensor& cache, int64_t H,
-                            int64_t pos, const c10::optional<at::Tensor>& pos_dev) {
+                            int64_t pos, const c10::optional<at::Tensor>& pos_dev,
+                            const c10::optional<at::Tensor>& part,
+                            const c10::optional<at::Tensor>& counters) {
   CHECK_BF16(qkv_new); CHECK_BF16(cache); CHECK_CONTIG(qkv_new); CHECK_CONTIG(cache);
   TORCH_CHECK(cache.dim() == 3, "cache must be [B, Tmax, 3D]");
   const int64_t B = cache.size(0), Tmax = cache.size(1), D3 = cache.size(2), D = D3 / 3;
@@ -531,8 +546,22 @@ at::Tensor attention_decode(const at::Tensor& qkv_new, const at::Tensor& cache, 
     TORCH_CHECK(pos_dev->scalar_type() == at::kInt && pos_dev->is_cuda(), "pos_dev must be int32 cuda");
     pd = pos_dev->data_ptr<int>();
   }
+  const int64_t np = (int64_t)mg::attention_decode_part_floats((int)B, (int)H, (int)(D / H));
+  at::Tensor pt, ct;
+  if (part.has_value() && part->defined()) {
+    TORCH_CHECK(counters.has_value() && counters->defined(), "attention_decode: part without counters");
+    CHECK_F32(*part); CHECK_DEV(*counters);
+    TORCH_CHECK(part->numel() >= np && part->device() == cache.device(), "attention_decode: part workspace too small");
+    TORCH_CHECK(counters->scalar_type() == at::kInt && counters->numel() >= B * H &&
+                counters->device() == cache.device(), "attention_decode: counters must be int32 [B * H]");
+    pt = *part;
+    ct = *counters;
+  } else {
+    pt = at::empty({np}, cache.options().dtype(at::kFloat));
+    ct = at::zeros({B * H}, cache.options().dtype(at::kInt));
+  }
   mg::attention_decode(bp(qkv_new), bp(cache), bp(out), (int)B, (int)H, (int)(D / H), Tmax, (int)pos,
-                       cur_stream(), pd);
+                       cur_stream(), fp(pt), reinterpret_cast<unsigned*>(ct.data_ptr<int>()), pd);
   return out;
 }
 
@@ -591,5 +620,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("N"), py::arg("B"));
   m.def("gemv_supported", &mg::gemv_supported);
   m.def("attention_decode", &attention_decode, py::arg("qkv_new"), py::arg("cache"), py::arg("H"),
-        py::arg("pos"), py::arg("pos_dev") = py::none());
+        py::arg("pos"), py::arg("pos_dev") = py::none(), py::arg("part") = py::none(),
+        py::arg("counters") = py::none());
+  m.def("attention_decode_part_floats", [](int64_t B, int64_t H, int64_t hd) {
+    return (int64_t)mg::attention_decode_part_floats((int)B, (int)H, (int)hd);
+  });
 }

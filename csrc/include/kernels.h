@@ -120,9 +120,13 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
                    int hd, float p, uint64_t seed, hipStream_t stream, float* dbias = nullptr,
                    bool delta_ready = false);  // delta already holds rowsum(dO * O) (gemm EPI 5)
 
-// one decode step: appends K/V of qkv_new [B, 3D] at row pos of cache [B, Tmax, 3D]; out [B, D]
+// one decode step: appends K/V of qkv_new [B, 3D] at row pos of cache [B, Tmax, 3D]; out [B, D].
+// part (attention_decode_part_floats(B, H, hd) floats) and counters (B * H, zero; the kernel leaves
+// them zero) are the caller's workspace: one per decode state, so a captured hipGraph never sees
+// another state's (possibly freed) buffers.
+size_t attention_decode_part_floats(int B, int H, int hd);
 void attention_decode(const bf16_t* qkv_new, bf16_t* cache, bf16_t* out, int B, int H, int hd,
-                      long Tmax, int pos, hipStream_t stream,
+                      long Tmax, int pos, hipStream_t stream, float* part, unsigned* counters,
                       const int* pos_dev = nullptr);
 
 }  // namespace mg

@@ -180,31 +180,20 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
 
 namespace mg {
 
-// persistent decode workspace: per-split partial states and per-(b, h) counters (zeroed once;
-// the kernel leaves them zero), grown on demand outside graph capture (the warm-up step runs first)
-static float* g_dec_part = nullptr;
-static unsigned* g_dec_cnt = nullptr;
-static size_t g_dec_part_n = 0, g_dec_cnt_n = 0;
+size_t attention_decode_part_floats(int B, int H, int hd) {
+  return (size_t)B * H * kDecSplitsMax * (hd + 2);
+}
 
+// part / counters: the caller's workspace (kernels.h).  They used to be one process-wide buffer
+// grown on demand, which a decode hipGraph captured at a smaller size then replayed into freed
+// memory once another batch size had re-allocated it.
 void attention_decode(const bf16_t* qkv_new, bf16_t* cache, bf16_t* out, int B, int H, int hd,
-                      long Tmax, int pos, hipStream_t stream, const int* pos_dev) {
+                      long Tmax, int pos, hipStream_t stream, float* part, unsigned* counters,
+                      const int* pos_dev) {
   // fixed grid (graph replays move pos only); the kernel uses ceil(L / 128) of the S splits, so
   // each holds <= 256 keys for Tmax <= 4096 (checked by the binding)
   const int S = kDecSplitsMax;
   const int CH = 0;
-  const size_t np = (size_t)B * H * S * (hd + 2), nc = (size_t)B * H;
-  if (np > g_dec_part_n) {
-    if (g_dec_part) hipFree(g_dec_part);
-    hipMalloc(&g_dec_part, np * sizeof(float));
-    g_dec_part_n = np;
-  }
-  if (nc > g_dec_cnt_n) {
-    if (g_dec_cnt) hipFree(g_dec_cnt);
-    hipMalloc(&g_dec_cnt, nc * sizeof(unsigned));
-    hipMemset(g_dec_cnt, 0, nc * sizeof(unsigned));
-    hipDeviceSynchronize();
-    g_dec_cnt_n = nc;
-  }
   // keys per split: a split hands its partial state to the last arrival (store drain + returning
   // atomic, ~5 us measured when 48 workgroups meet on one counter); with few (b, h) pairs a single
   // workgroup up to 256 keys beats splitting (B = 1 greedy: 3,167 -> 3,289 tok/s), with many the
@@ -212,7 +201,7 @@ void attention_decode(const bf16_t* qkv_new, bf16_t* cache, bf16_t* out, int B, 
   const int kps = B * H <= 32 ? 256 : 128;
   attn_decode_kernel<<<B * H * S, 256, 0, stream>>>(qkv_new, cache, out, H, hd, H * hd, Tmax, pos, pos_dev,
                                                     1.4426950408889634f / sqrtf((float)hd), S, CH, kps,
-                                                    g_dec_part, g_dec_cnt);
+                                                    part, counters);
 }
 
 }  // namespace mg

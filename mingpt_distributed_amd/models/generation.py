@@ -20,6 +20,7 @@ import torch
 import torch.nn.functional as F
 
 from ..ops import reference as R
+from ..ops.grads import before_use
 
 
 def _sample(logits, temperature, do_sample, top_k):
@@ -128,6 +129,12 @@ class _GpuCache:
         self.B = B
         self.caches = [torch.empty(B, tmax, 3 * D, device=idx.device, dtype=torch.bfloat16)
                        for _ in range(cfg.n_layer)]
+        # decode-attention workspace owned by this state (split partials + per-(b, h) counters
+        # that the kernel leaves zero): the captured graphs bake these pointers in
+        H = cfg.n_head
+        self.dec_part = torch.empty(self.C.attention_decode_part_floats(B, H, D // H),
+                                    device=idx.device, dtype=torch.float32)
+        self.dec_cnt = torch.zeros(B * H, device=idx.device, dtype=torch.int32)
         self.stamp = _weight_stamp(model)
         self.logits = self._run(idx, 0)
 
@@ -189,7 +196,7 @@ class _GpuCache:
                 self.caches[i][:, :T].copy_(qkv.view(B, T, 3 * D))
                 y, _, _ = C.attention_fwd(qkv, B, T, H, 0.0, 0)
             else:
-                y = C.attention_decode(qkv, self.caches[i], H, pos0, pos_dev)
+                y = C.attention_decode(qkv, self.caches[i], H, pos0, pos_dev, self.dec_part, self.dec_cnt)
             x = lin(y, a.c_proj.weight, a.c_proj.bias, "resid", resid=x)
             u = lin(x, mm.c_fc.weight, mm.c_fc.bias, "gelu", ln=blk.ln_2)
             x = lin(u, mm.c_proj.weight, mm.c_proj.bias, "resid", resid=x)
@@ -306,6 +313,10 @@ _GRAPH_DECODE = True  # set False to launch the decode step eagerly
 def generate(model, idx, max_new_tokens: int, temperature: float = 1.0, do_sample: bool = False,
              top_k: Optional[int] = None, use_cache: bool = True):
     bs = model.block_size
+    # ZeRO-1: the KV-cache path launches the kernels directly (never model.forward), so neither
+    # the fused ops' per-bucket waits nor the engine's forward pre-hook run: wait here for every
+    # in-flight parameter all-gather (stream-ordered) before any decode kernel reads the weights
+    before_use(*model.parameters())
     if not use_cache:
         for _ in range(max_new_tokens):
             idx_cond = idx if idx.size(1) <= bs else idx[:, -bs:]

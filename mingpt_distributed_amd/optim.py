@@ -16,7 +16,7 @@
 from __future__ import annotations
 
 import math
-from typing import Dict, List, Optional, Set, Tuple
+from typing import Dict, List, NamedTuple, Optional, Set, Tuple
 
 import torch
 import torch.nn as nn
@@ -71,23 +71,41 @@ def _round_up(n: int, m: int) -> int:
     return (n + m - 1) // m * m
 
 
-def make_chunk_table(pieces, device, bound: int, moment_bound: Optional[int] = None):
+class ChunkTable(NamedTuple):
+    """Device chunk table of the multi-tensor kernels plus the bounds it was validated against:
+    ``end`` = one past the last flat-buffer element any chunk touches, ``mend`` = the same for the
+    (packed) moment buffers.  The bindings check the buffers they are handed against these, so a
+    table built for another store (e.g. before a re-layout) fails loudly instead of indexing out
+    of bounds."""
+    start: torch.Tensor
+    len: torch.Tensor
+    wd: torch.Tensor
+    mstart: torch.Tensor
+    end: int
+    mend: int
+
+
+def make_chunk_table(pieces, device, bound: int, moment_bound: Optional[int] = None) -> ChunkTable:
     """Kernel chunk table from ``pieces`` = [(start, end, wd, moment_start)] of flat-buffer ranges:
     CHUNK-sized chunks (one workgroup each) that never straddle a piece, so weight decay is a
     per-chunk constant.  Every range is checked against the buffers here, on the host, because
     the kernels index the flat buffers through these tables unchecked."""
     starts, lens, wds, mstarts = [], [], [], []
+    end = mend = 0
     for a, b, wd, ma in pieces:
         if not (0 <= a <= b <= bound) or a % 4 or (ma is not None and (ma % 4 or ma + (b - a) > moment_bound)):
             raise ValueError(f"chunk piece [{a}, {b}) (moments at {ma}) outside the flat buffers")
+        end = max(end, b)
+        mend = max(mend, (a if ma is None else ma) + (b - a))
         for c in range(a, b, CHUNK):
             starts.append(c)
             lens.append(min(CHUNK, b - c))
             wds.append(wd)
             mstarts.append(c - a + (a if ma is None else ma))
     t = dict(device=device)
-    return (torch.tensor(starts, dtype=torch.int64, **t), torch.tensor(lens, dtype=torch.int32, **t),
-            torch.tensor(wds, dtype=torch.float32, **t), torch.tensor(mstarts, dtype=torch.int64, **t))
+    return ChunkTable(torch.tensor(starts, dtype=torch.int64, **t), torch.tensor(lens, dtype=torch.int32, **t),
+                      torch.tensor(wds, dtype=torch.float32, **t), torch.tensor(mstarts, dtype=torch.int64, **t),
+                      end, mend)
 
 
 class FlatParamStore:
@@ -206,8 +224,8 @@ class FusedAdamW:
         self.exp_avg_sq = torch.zeros(store.total, dtype=torch.float32, device=dev)
         self.norm_buf = torch.zeros(2, dtype=torch.float32, device=dev)
         pieces = [(a, b, wd, None) for a, b, wd in store.pieces(self.wd_of)]
-        self.c_start, self.c_len, self.c_wd, _ = make_chunk_table(pieces, dev, store.total)
-        self.n_chunks = int(self.c_len.numel())
+        self.table = make_chunk_table(pieces, dev, store.total)
+        self.n_chunks = int(self.table.len.numel())
         # where step() reads the (all-reduced) gradients: the fp32 main grads, or the bf16 buffer
         # the data-parallel engine reduced them in (DataParallelEngine(reduce_dtype=bf16))
         self.grad_buffer: torch.Tensor = store.grad
@@ -228,10 +246,11 @@ class FusedAdamW:
             from .ops._ext import ext
 
             C = ext()
-            C.grad_sumsq_chunks(self.c_start, self.c_len, self.grad_buffer, grad_scale, self.norm_buf)
-            C.adamw_step(self.c_start, self.c_len, self.c_wd, None, s.master, s.flat, self.grad_buffer,
+            t = self.table
+            C.grad_sumsq_chunks(t.start, t.len, self.grad_buffer, grad_scale, self.norm_buf, t.end)
+            C.adamw_step(t.start, t.len, t.wd, None, s.master, s.flat, self.grad_buffer,
                          self.exp_avg, self.exp_avg_sq, self.norm_buf, lr, b1, b2, self.eps,
-                         self.step_count, grad_scale, float(self.grad_clip))
+                         self.step_count, grad_scale, float(self.grad_clip), t.end, t.mend)
             return
         # CPU path (plain PyTorch, same math)
         g = self.grad_buffer.float() * grad_scale

@@ -201,14 +201,39 @@ class DataParallelEngine:
 
     def relayout_order(self) -> Optional[List[str]]:
         """Parameter names in observed gradient-ready order if that differs from the layout
-        (buckets would wait on late gradients), else None.  Consumed once."""
+        (buckets would wait on late gradients), else None.  Consumed once.
+
+        Collective (once, at the step after the first synchronised backward, which is the same
+        step on every rank) when the engine communicates: each rank observes its OWN order, and
+        ranks whose bucket boundaries differed would issue collectives of different sizes (hang
+        or silent corruption), so rank 0's decision is broadcast and every rank adopts it."""
         obs, self.observed = self.observed, None
         if obs is None:
             return None
+        order = None
         seq = [self.bucket_of[i] for i in obs]
-        if all(a <= b for a, b in zip(seq, seq[1:])):
-            return None  # buckets complete in launch order; order inside a bucket is irrelevant
-        return [self.store.names[i] for i in obs]
+        # buckets complete in launch order: order inside a bucket is irrelevant
+        if not all(a <= b for a, b in zip(seq, seq[1:])):
+            order = [self.store.names[i] for i in obs]
+        if self.active and self.world > 1:
+            box = [order]
+            src = dist.get_global_rank(self.pg, 0) if self.pg is not None else 0
+            dist.broadcast_object_list(box, src=src, group=self.pg)
+            order = box[0]
+            if order is not None and sorted(order) != sorted(self.store.names):
+                raise RuntimeError("relayout_order: rank 0's parameter order names other parameters")
+        return order
+
+    def comm_plan(self) -> dict:
+        """What one synchronised step puts on the wire (bench/diagnostics): bucket count, bytes
+        of every bucket in launch order (wire dtype), the collective kind."""
+        esz = 2 if self.reduce_dtype == torch.bfloat16 else 4
+        return {"n_buckets": len(self.buckets),
+                "bucket_bytes": [(b.end - b.start) * esz for b in self.buckets],
+                "wire_dtype": "bf16" if esz == 2 else "fp32",
+                "collective": self.collective_kind}
+
+    collective_kind = "all_reduce"
 
     @contextlib.contextmanager
     def no_sync(self):

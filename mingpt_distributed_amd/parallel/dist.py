@@ -43,8 +43,11 @@ def env_ranks():
     return rank, world, local
 
 
-def init_distributed(device: str = "auto", backend: str = "auto", timeout_s: int = 1800) -> DistInfo:
-    """Initialise (idempotent).  ``device``: auto|cuda|cpu.  ``backend``: auto|nccl|gloo."""
+def init_distributed(device: str = "auto", backend: str = "auto", timeout_s: int = 1800,
+                     group_at_world1: bool = False) -> DistInfo:
+    """Initialise (idempotent).  ``device``: auto|cuda|cpu.  ``backend``: auto|nccl|gloo.
+    ``group_at_world1``: create a one-rank process group even without a torchrun env (drives the
+    RCCL calls on one GPU: plumbing checks of the collective path, ``comm_at_world1`` engines)."""
     global _INFO
     rank, world, local = env_ranks()
     if device == "auto":
@@ -56,8 +59,16 @@ def init_distributed(device: str = "auto", backend: str = "auto", timeout_s: int
         dev = torch.device("cpu")
     if backend == "auto":
         backend = "nccl" if dev.type == "cuda" else "gloo"
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or group_at_world1) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1 and "MASTER_PORT" not in os.environ:
+            import socket
+
+            with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+                sk.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kw["device_id"] = dev
@@ -72,7 +83,7 @@ def init_distributed(device: str = "auto", backend: str = "auto", timeout_s: int
             kw.update(store=dist.PrefixStore(f"mingpt/attempt{restart}", base), rank=rank, world_size=world)
         dist.init_process_group(**kw)
     _INFO = DistInfo(rank=rank, world_size=world, local_rank=local, device=dev,
-                     backend=backend if world > 1 else "none")
+                     backend=backend if (world > 1 or dist.is_initialized()) else "none")
     return _INFO
 
 

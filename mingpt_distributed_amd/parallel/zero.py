@@ -22,7 +22,9 @@ This is that step, built on the same flat buffers and bucket layout as
   (input = own slice of the output), asynchronously.  The next forward waits per bucket, right
   before the first kernel that reads one of its weights (``ops/grads.before_use``): the gather of
   later layers overlaps the forward of earlier ones.  Forwards that do not go through the fused
-  GPU ops (CPU path, ``no_grad`` inference, generation) wait for everything up front.
+  GPU ops (CPU path, ``no_grad`` inference, models other than this package's GPT) wait for
+  everything up front in a forward pre-hook; ``generate`` (whose KV-cache decode calls the
+  kernels directly, never ``model.forward``) waits through ``before_use`` on every parameter.
 * **Snapshots.**  The fp32 master is replicated in memory, but only the rank's pieces are
   current: :meth:`ZeroAdamW.consolidate` (collective) all-gathers masters in place (no extra
   memory) and streams each bucket's moment slices to rank 0, which copies them to host memory.
@@ -44,6 +46,8 @@ from .ddp import DataParallelEngine, _Bucket
 
 class ZeroGradEngine(DataParallelEngine):
     """Gradient and parameter side of ZeRO-1 (see module docstring)."""
+
+    collective_kind = "reduce_scatter + all_gather (bf16 params)"
 
     def __init__(self, store: FlatParamStore, process_group=None, broadcast: bool = True,
                  reduce_dtype: Optional[torch.dtype] = None, model: Optional[torch.nn.Module] = None,
@@ -67,6 +71,15 @@ class ZeroGradEngine(DataParallelEngine):
         # reduce-scatter: it all-reduces the whole bucket (2x the traffic, same result)
         self._gloo = multi and dist.get_backend(process_group) == "gloo"
         self._hook_handle = None
+        # Per-bucket waits are only sound when every weight read of a grad-enabled GPU forward
+        # goes through a fused op that calls ``ops.grads.before_use`` first: the contract holds
+        # for this package's GPT.forward (ops/fused.py) and is not assumed for anything else (a
+        # subclass overriding forward, custom heads, user modules): those wait for everything.
+        self._fused_forward = False
+        if model is not None:
+            from ..models.gpt import GPT
+
+            self._fused_forward = isinstance(model, GPT) and type(model).forward is GPT.forward
         if multi and model is not None:
             self._hook_handle = model.register_forward_pre_hook(self._forward_pre_hook)
 
@@ -122,7 +135,8 @@ class ZeroGradEngine(DataParallelEngine):
 
     def _forward_pre_hook(self, module, args):
         idx = args[0] if args else None
-        if not (isinstance(idx, torch.Tensor) and idx.is_cuda and torch.is_grad_enabled()):
+        if not (self._fused_forward and isinstance(idx, torch.Tensor) and idx.is_cuda
+                and torch.is_grad_enabled()):
             self.wait_gathers()
 
     def all_gather_inplace(self, buf: torch.Tensor):
@@ -172,9 +186,8 @@ class ZeroAdamW(FusedAdamW):
         for (lo, hi), mo in zip(engine.own, self.moff):
             for a, b, wd in store.pieces(self.wd_of, lo, hi):
                 self.pieces.append((a, b, wd, mo + (a - lo)))
-        self.c_start, self.c_len, self.c_wd, self.c_mstart = make_chunk_table(
-            self.pieces, dev, store.total, off)
-        self.n_chunks = int(self.c_len.numel())
+        self.table = make_chunk_table(self.pieces, dev, store.total, off)
+        self.n_chunks = int(self.table.len.numel())
         self._host_state = None
         self.param_groups = [{"lr": lr, "betas": self.betas, "weight_decay": weight_decay, "eps": eps}]
 
@@ -201,12 +214,13 @@ class ZeroAdamW(FusedAdamW):
             from ..ops._ext import ext
 
             C = ext()
-            C.grad_sumsq_chunks(self.c_start, self.c_len, g, grad_scale, self.norm_buf)
+            t = self.table
+            C.grad_sumsq_chunks(t.start, t.len, g, grad_scale, self.norm_buf, t.end)
             self._all_reduce_sumsq()
             torch.mul(self.norm_buf[:1].sqrt(), grad_scale, out=self.norm_buf[1:])
-            C.adamw_step(self.c_start, self.c_len, self.c_wd, self.c_mstart, s.master, s.flat, g,
+            C.adamw_step(t.start, t.len, t.wd, t.mstart, s.master, s.flat, g,
                          self.exp_avg, self.exp_avg_sq, self.norm_buf, lr, b1, b2, self.eps,
-                         self.step_count, grad_scale, float(self.grad_clip))
+                         self.step_count, grad_scale, float(self.grad_clip), t.end, t.mend)
             e.gather_params()
             return
         # CPU path (same math as FusedAdamW's, on the owned pieces)

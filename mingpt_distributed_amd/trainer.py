@@ -99,6 +99,8 @@ class StepEngine:
         self.world = self.dp.world if self.dp else 1
         self._hooks = []
         self.annotate = False  # record_function ranges (fwd/bwd/allreduce/optim) while profiling
+        self.measure_comm = False  # hipEvents around dp.finish() (comm_exposed_ms)
+        self._comm_events = []
         self._fold_hooks()
 
     def _fold_hooks(self):
@@ -177,9 +179,29 @@ class StepEngine:
             with self._range("mingpt::backward"):
                 (loss * scale if scale != 1.0 else loss).backward()
             if self.dp is not None:
+                ev = None
+                if self.measure_comm and sync and self.device.type == "cuda":
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    ev[0].record()  # after the last backward kernel on the compute stream
                 with self._range("mingpt::allreduce_wait"):
                     self.dp.finish()
+                if ev is not None:
+                    ev[1].record()  # the compute stream has waited for every outstanding collective
+                    self._comm_events.append(ev)
         return loss.detach()
+
+    def comm_exposed_ms(self, reset: bool = True) -> Optional[float]:
+        """Mean device time, over the synchronised steps since the last call, from the end of
+        backward's last kernel to the end of ``dp.finish()`` (the gradient communication NOT
+        hidden under backward).  Needs ``measure_comm = True`` beforehand; synchronises the
+        device; None when nothing was recorded (no data-parallel engine, CPU)."""
+        evs = self._comm_events
+        if reset:
+            self._comm_events = []
+        if not evs:
+            return None
+        torch.cuda.synchronize(self.device)
+        return sum(a.elapsed_time(b) for a, b in evs) / len(evs)
 
     def optimizer_step(self):
         with self._range("mingpt::optimizer"):

@@ -8,6 +8,7 @@ Checks: the all-reduced gradient of a 2-rank step equals the 1-process gradient 
 concatenated batch (also with gradient accumulation), and the ranks stay bit-identical over
 several optimizer steps.
 """
+import math
 import os
 import socket
 
@@ -191,8 +192,14 @@ def _worker_rccl1(port, out_dir, zero1, bf16):
                      reduce_dtype=torch.bfloat16 if bf16 else None, comm_at_world1=True)
     assert eng.dp is not None and eng.dp.active and len(eng.dp.buckets) > 3
     x, y = _batch()
+    eng.measure_comm = True  # bench.py's comm_exposed_ms plumbing on the real RCCL path
     for _ in range(3):
         eng.train_step([(x.cuda(), y.cuda())])
+    c = eng.comm_exposed_ms()
+    assert c is not None and math.isfinite(c) and c >= 0.0, c
+    plan = eng.dp.comm_plan()
+    assert plan["n_buckets"] == len(eng.dp.buckets) and len(plan["bucket_bytes"]) == plan["n_buckets"]
+    assert plan["wire_dtype"] == ("bf16" if bf16 else "fp32")
     if zero1:
         eng.opt.consolidate()
         st = eng.opt.state_dict()
@@ -200,6 +207,47 @@ def _worker_rccl1(port, out_dir, zero1, bf16):
     torch.cuda.synchronize()
     torch.save(eng.model_state_dict(), os.path.join(out_dir, "rccl1.pt"))
     dist.destroy_process_group()
+
+
+def _worker_zero1_generate(port, out_dir):
+    """ZeRO-1 on a one-rank RCCL group (collective path forced): generate() right after an
+    optimizer step, while the parameter all-gathers are in flight, must decode from the gathered
+    weights: the same tokens as a plain copy of the trained weights."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from mingpt_distributed_amd.models import GPT
+    from mingpt_distributed_amd.trainer import StepEngine
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    model = _model()
+    eng = StepEngine(model, lr=1e-3, grad_clip=1.0, device=dev, bucket_mb=0.5, zero1=True,
+                     comm_at_world1=True)
+    x, y = _batch()
+    eng.train_step([(x.cuda(), y.cuda())])
+    model.eval()
+    idx = x[:1, :5].cuda()
+    out = model.generate(idx, 12, do_sample=False)
+    torch.cuda.synchronize()
+    ref = GPT(model.config, verbose=False).to(dev).to(torch.bfloat16).eval()
+    ref.load_state_dict({k: v.to(torch.bfloat16) for k, v in eng.model_state_dict().items()})
+    torch.save({"out": out.cpu(), "ref": ref.generate(idx, 12, do_sample=False).cpu()},
+               os.path.join(out_dir, "zgen.pt"))
+    dist.destroy_process_group()
+
+
+def test_gpu_zero1_generate_after_step(tmp_path):
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_worker_zero1_generate, args=(_port(), str(tmp_path)))
+    p.start()
+    p.join(timeout=100)
+    if p.is_alive():
+        p.kill()
+    assert p.exitcode == 0, p.exitcode
+    r = torch.load(tmp_path / "zgen.pt", weights_only=True)
+    assert torch.equal(r["out"], r["ref"])
 
 
 @pytest.mark.parametrize("zero1,bf16", [(False, False), (False, True), (True, False), (True, True)])

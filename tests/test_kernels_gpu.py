@@ -150,7 +150,8 @@ def test_adamw_matches_torch():
         opt.step()
         C.grad_sumsq(g, 1.0, norm)
         torch.testing.assert_close(norm[1], total, rtol=1e-4, atol=1e-4)
-        C.adamw_step(cs, cl, cw, None, master, param, g, m, v, norm, 1e-3, 0.9, 0.95, 1e-8, step, 1.0, 1.0)
+        C.adamw_step(cs, cl, cw, None, master, param, g, m, v, norm, 1e-3, 0.9, 0.95, 1e-8, step, 1.0, 1.0,
+                     n, n)
     torch.testing.assert_close(master, torch.cat([p.detach() for p in ref_params]), atol=1e-5, rtol=1e-4)
     _close(param, master, atol=1e-2)
 
@@ -167,7 +168,9 @@ def test_adamw_pieces_packed_moments(gdtype):
     n = 200_000
     pieces = [(0, 40_000, 0.1, 0), (70_016, 140_032, 0.0, 40_000), (150_016, 199_936, 0.1, 110_016)]
     nm = sum(b - a for a, b, _, _ in pieces)
-    cs, cl, cw, cm = make_chunk_table(pieces, DEV, n, nm)
+    t = make_chunk_table(pieces, DEV, n, nm)
+    cs, cl, cw, cm = t.start, t.len, t.wd, t.mstart
+    assert (t.end, t.mend) == (199_936, nm)
     master = torch.randn(n, device=DEV)
     param = master.to(torch.bfloat16)
     g = torch.randn(n, device=DEV).to(gdtype)
@@ -177,11 +180,12 @@ def test_adamw_pieces_packed_moments(gdtype):
     norm = torch.zeros(2, device=DEV)
     lr, b1, b2, eps, gs, clip = 1e-3, 0.9, 0.95, 1e-8, 0.5, 1.0
     for step in range(1, 3):
-        C.grad_sumsq_chunks(cs, cl, g, gs, norm)
+        C.grad_sumsq_chunks(cs, cl, g, gs, norm, t.end)
         gf = g.float()
         sq = sum((gf[a:b] * gs).pow(2).sum() for a, b, _, _ in pieces)
         torch.testing.assert_close(norm[1], sq.sqrt(), rtol=1e-4, atol=1e-4)
-        C.adamw_step(cs, cl, cw, cm, master, param, g, m, v, norm, lr, b1, b2, eps, step, gs, clip)
+        C.adamw_step(cs, cl, cw, cm, master, param, g, m, v, norm, lr, b1, b2, eps, step, gs, clip,
+                     t.end, t.mend)
         coef = min(1.0, clip / (sq.sqrt().item() + 1e-6))
         for a, b, wd, ma in pieces:
             gg = gf[a:b] * gs * coef
@@ -196,6 +200,12 @@ def test_adamw_pieces_packed_moments(gdtype):
     torch.testing.assert_close(v, ref_v, atol=1e-7, rtol=1e-4)
     with pytest.raises(ValueError):
         make_chunk_table([(0, n + 64, 0.0, None)], DEV, n)
+    # a table validated against larger buffers than the ones handed in fails in the binding
+    with pytest.raises(RuntimeError, match="chunk table"):
+        C.grad_sumsq_chunks(cs, cl, g[:100_000], gs, norm, t.end)
+    with pytest.raises(RuntimeError, match="chunk table"):
+        C.adamw_step(cs, cl, cw, cm, master, param, g, m[:1000], v[:1000], norm, lr, b1, b2, eps, 3, gs,
+                     clip, t.end, t.mend)
 
 
 @pytest.mark.parametrize("N", [768, 2304, 3072, 520])  # 32- and 64-lane bias-grad row chunks

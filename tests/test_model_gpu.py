@@ -132,6 +132,22 @@ def test_greedy_device_loop_matches_host_argmax():
     assert torch.equal(a[:, T0:T0 + n + 1], torch.stack(toks, 1))
 
 
+def test_decode_graphs_of_two_models_do_not_share_workspace():
+    """Model A captures its decode graphs at B = 1, model B then decodes at B = 8 (a larger
+    decode-attention workspace), then A replays its graphs: A's tokens must not change.  The
+    workspace used to be one process-wide buffer re-allocated for B's size, leaving A's captured
+    graph writing into freed memory."""
+    torch.manual_seed(0)
+    a = GPT(_cfg(block_size=64), verbose=False).cuda().to(torch.bfloat16).eval()
+    b = GPT(_cfg(block_size=64, n_head=4), verbose=False).cuda().to(torch.bfloat16).eval()
+    ia = torch.randint(0, 1000, (1, 6), device="cuda")
+    ib = torch.randint(0, 1000, (8, 6), device="cuda")
+    first = a.generate(ia, 40, do_sample=False)
+    b.generate(ib, 40, do_sample=False)
+    again = a.generate(ia, 40, do_sample=False)
+    assert torch.equal(first, again)
+
+
 def test_gpt2_shape_step():
     """Full GPT-2 layer shapes (D=768, H=12, hd=64) at a short sequence through the engine."""
     torch.manual_seed(0)
