@@ -1,11 +1,13 @@
 #!/usr/bin/env python
 """Loss parity of bf16 vs fp32 gradient reduction (DataParallelEngine ``reduce_dtype``).
 
-Two data-parallel ranks (gloo on CPU, or ``--device cuda`` with both ranks on one card) train the
+``--world`` data-parallel ranks (default 2; 8 = one MI355X node; gloo on CPU, or ``--device cuda``
+with every rank on one card) train the
 same gpt-mini char-LM from the same init on the same rank-sharded batches, once with fp32 and once
 with bf16 gradients on the wire; the per-step losses are written as JSON lines.
 
     python bench/reduce_dtype_parity.py --steps 200 --out profiles/round2_reduce_dtype_parity.jsonl
+    python bench/reduce_dtype_parity.py --world 8 --batch 4 --steps 60 --out profiles/round3_reduce_dtype_parity_8rank_cpu.jsonl
 """
 import argparse
 import json
@@ -41,7 +43,7 @@ def _worker(rank, world, port, a, reduce, q):
     from mingpt_distributed_amd.parallel import dist as D
     from mingpt_distributed_amd.trainer import StepEngine
 
-    torch.set_num_threads(2)
+    torch.set_num_threads(max(1, 8 // world))
     D.init_distributed(device=a.device, backend="gloo")
     text = _text()
     chars = sorted(set(text))
@@ -72,6 +74,7 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--block", type=int, default=64)
     ap.add_argument("--device", default="cpu")
+    ap.add_argument("--world", type=int, default=2)
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     ctx = mp.get_context("spawn")
@@ -79,7 +82,7 @@ def main():
     for reduce in ("fp32", "bf16"):
         q = ctx.Queue()
         port = _port()
-        ps = [ctx.Process(target=_worker, args=(r, 2, port, a, reduce, q)) for r in range(2)]
+        ps = [ctx.Process(target=_worker, args=(r, a.world, port, a, reduce, q)) for r in range(a.world)]
         for p in ps:
             p.start()
         res[reduce] = q.get()
@@ -89,7 +92,7 @@ def main():
     for i in range(a.steps):
         lines.append({"step": i, "loss_fp32": res["fp32"][i], "loss_bf16": res["bf16"][i]})
     k = max(1, a.steps // 10)
-    summ = {"summary": True, "device": a.device, "world": 2, "steps": a.steps,
+    summ = {"summary": True, "device": a.device, "world": a.world, "batch_per_rank": a.batch, "steps": a.steps,
             "final_fp32": sum(res["fp32"][-k:]) / k, "final_bf16": sum(res["bf16"][-k:]) / k,
             "max_abs_diff": max(abs(u - v) for u, v in zip(res["fp32"], res["bf16"]))}
     print(json.dumps(summ))
