@@ -62,6 +62,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True, debug: bool 
     ``-DMG_DEBUG`` (device-side range checks on token ids / targets, common.h MG_CHECK_INDEX) into
     ``build/debug/_C.so``; load it with ``MINGPT_EXT_SO=build/debug/_C.so MINGPT_DEBUG_CHECKS=1``."""
     flags = COMMON_FLAGS + (["-DMG_DEBUG"] if debug else [])
+    flags += os.environ.get("MG_EXTRA_FLAGS", "").split()  # kernel variant switches (A/B builds)
     bdir = BUILD + "_debug" if debug else BUILD
     os.makedirs(bdir, exist_ok=True)
     headers = glob.glob(os.path.join(ROOT, "csrc", "include", "*.h"))
@@ -103,16 +104,44 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True, debug: bool 
     return out
 
 
+def _torch_runtime_dir() -> str:
+    """build/torchlibs: links, under their sonames, to the HIP runtime and RCCL that torch ships
+    (torch/lib holds them as libamdhip64.so / librccl.so, so a NEEDED libamdhip64.so.7 /
+    librccl.so.1 would otherwise resolve to /opt/rocm's).  Native tools link and run against
+    these: the RCCL they time is the one training loads (2.26.6 here, not /opt/rocm's 2.27.7),
+    and one HIP runtime per process."""
+    _, tlib, _ = _torch_paths()
+    d = os.path.join(ROOT, "build", "torchlibs")
+    os.makedirs(d, exist_ok=True)
+    # torch's RCCL asks for the unversioned names of its own dependencies; point those at torch's
+    # files too, so the process maps each runtime library once
+    names = [("libamdhip64.so", "libamdhip64.so.7"), ("libamdhip64.so", "libamdhip64.so"),
+             ("librccl.so", "librccl.so.1")]
+    names += [(n, n) for n in ("libhsa-runtime64.so", "libroctx64.so", "librocm_smi64.so",
+                               "librocprofiler-register.so") if os.path.exists(os.path.join(tlib, n))]
+    for name, soname in names:
+        link = os.path.join(d, soname)
+        target = os.path.join(tlib, name)
+        if os.path.lexists(link) and os.readlink(link) != target:
+            os.remove(link)
+        if not os.path.lexists(link):
+            os.symlink(target, link)
+    return d
+
+
 def build_tools(verbose: bool = True):
-    """Native tools (standalone executables against /opt/rocm HIP + RCCL)."""
+    """Native tools (standalone executables: HIP + the RCCL bundled with torch, see
+    _torch_runtime_dir)."""
     outdir = os.path.join(ROOT, "build", "bin")
     os.makedirs(outdir, exist_ok=True)
+    tdir = _torch_runtime_dir()
     built = []
     for src in sorted(glob.glob(os.path.join(ROOT, "tools", "*.cpp"))):
         exe = os.path.join(outdir, os.path.splitext(os.path.basename(src))[0])
-        if _newer(exe, [src]):
+        if _newer(exe, [src, os.path.abspath(__file__)]):
             _run([HIPCC, "-O2", "-std=c++17", f"--offload-arch={ARCH}", "-x", "hip", "-o", exe, src,
-                  "-I/opt/rocm/include", "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"])
+                  "-I/opt/rocm/include", "-L" + tdir, "-l:librccl.so.1", "-l:libamdhip64.so.7",
+                  "-Wl,--disable-new-dtags", "-Wl,-rpath," + tdir])
             if verbose:
                 print(f"[build_ext] built {os.path.relpath(exe, ROOT)}", flush=True)
         built.append(exe)

@@ -29,7 +29,7 @@ struct AttnArgs {
   float* dq;           // bwd fp32 dQ accumulator [B*T, D] (or per-key-block partials)
   long dq_part;        // bwd partial mode: elements between the per-key-block dQ partials (0: persistent)
   bf16_t* dqkv;        // bwd [B*T, 3D]
-  const uint32_t* dmask;  // dropout keep-bits, layout: attention_train.hip (mask kernel)
+  const uint32_t* dmask;  // dropout keep-bits, row words (attention_train.hip, mask kernel)
   int B, T, H, hd, D;
   float scale_log2;    // log2(e) / sqrt(hd)
   uint32_t thr;        // 8-bit keep threshold: keep iff random byte >= thr (0 = no dropout)

@@ -11,11 +11,16 @@
 //   5. an RCCL all-reduce over all local GPUs (ncclCommInitAll): correctness check, then a size
 //      sweep printing algorithm / bus bandwidth -- the numbers that size the gradient buckets;
 //   6. "hello from rank r on GPU g (bus id)" per rank.
+// Links the HIP runtime and RCCL that torch ships (build_ext._torch_runtime_dir), i.e. the RCCL the
+// training processes load, and reports its version and path.  With one visible GPU there is no
+// link to measure: the P2P and all-reduce bandwidth sections print "n/a" instead of timing no-ops.
 // Build: python build_ext.py --tools  ->  build/bin/xgmi_probe [--max-mb N] [--no-p2p]
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <hsa/hsa_ext_amd.h>
 #include <rccl/rccl.h>
+
+#include <dlfcn.h>
 
 #include <chrono>
 #include <cstdio>
@@ -92,7 +97,10 @@ int main(int argc, char** argv) {
   char host[256] = {0};
   gethostname(host, sizeof(host) - 1);
   const char* node = getenv("SLURM_NODEID");
-  printf("xgmi_probe on %s (node %s): %d GPU(s), RCCL %d\n", host, node ? node : "0", n, ver);
+  Dl_info di{};
+  const char* rpath = dladdr((void*)&ncclGetVersion, &di) && di.dli_fname ? di.dli_fname : "?";
+  printf("xgmi_probe on %s (node %s): %d GPU(s), RCCL %d.%d.%d (%s)\n", host, node ? node : "0", n,
+         ver / 10000, (ver / 100) % 100, ver % 100, rpath);
   std::vector<std::string> bus(n);
   for (int d = 0; d < n; ++d) {
     hipDeviceProp_t p;
@@ -140,6 +148,7 @@ int main(int argc, char** argv) {
     printf("  GPU %d device-local copy: %.0f GB/s (read+write %.0f GB/s)\n", d, gbs, 2 * gbs);
   }
   // ---- P2P bandwidth
+  if (n == 1) printf("P2P copy bandwidth: n/a (1 GPU visible: no xGMI link to measure)\n");
   if (p2p && n > 1) {
     for (int i = 0; i < n; ++i)
       for (int j = 0; j < n; ++j)
@@ -194,9 +203,12 @@ int main(int argc, char** argv) {
     for (float v : host) ok &= v == (float)(n * (n + 1) / 2);
   }
   printf("all-reduce correctness: %s\n", ok ? "OK" : "FAILED");
-  printf("all-reduce sweep (fp32 sum, %d ranks):\n  %10s %10s %12s %12s\n", n, "bytes", "time_us", "algbw_GB/s",
-         "busbw_GB/s");
-  for (size_t b = 1 << 20; b <= (max_mb << 20) && b <= bytes; b <<= 1) {
+  if (n == 1)
+    printf("all-reduce bandwidth: n/a (1 rank: the collective moves no data; run on a multi-GPU node)\n");
+  else
+    printf("all-reduce sweep (fp32 sum, %d ranks):\n  %10s %10s %12s %12s\n", n, "bytes", "time_us", "algbw_GB/s",
+           "busbw_GB/s");
+  for (size_t b = 1 << 20; n > 1 && b <= (max_mb << 20) && b <= bytes; b <<= 1) {
     const size_t c = b / 4;
     const int iters = 10;
     for (int w = 0; w < 2; ++w) {  // warm + timed
