@@ -419,7 +419,10 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restr
   }
 }
 
-constexpr int BQ = 64;  // queries per backward tile
+// queries per backward tile: 128 in key-block mode at hd 33..64 (two barriers per 128 queries, and
+// as many 32x32 dQ tiles as waves: no split-key dQ hand-off in LDS), else 64
+template <int NKS, bool PERSIST>
+constexpr int bwd_bq() { return (!PERSIST && (NKS == 3 || NKS == 4)) ? 128 : 64; }
 
 // In place on one 32x32 (query rows x key lanes) tile: s <- dropped P (dV operand), dp <- dS.
 // K is pre-scaled by c in LDS, so S' = Q (cK)^T - lse arrives in the log2 domain and p = exp2(S').
@@ -501,18 +504,22 @@ MG_DEVICE void tr_reduce32(float (&v)[NV], int lane) {
 //    same lane, so program order is the only ordering needed) and written as bf16 into dqkv by
 //    the last block that reaches the tile: no per-key-block partial buffers, no finalize pass.
 //  * attention dropout: the forward's keep bits (attn_dropmask_kernel), one word per query and
-//    32-key half tile, staged 64 queries x KW words per tile.
+//    32-key half tile, staged BQ queries x KW words per tile.
+//  * BQ = 128 queries per tile (key-block mode, hd <= 64): the dS^T image is two 64-query halves.
 template <int NKS, int KW, bool PERSIST>
 __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) {
+  constexpr int BQ = bwd_bq<NKS, PERSIST>();
+  constexpr int NQS = BQ / 32;                   // 32-query subtiles per tile
   constexpr int NH = (NKS + 3) / 4, NO = (NKS + 1) / 2;
   constexpr int NT = 64 * KW, KB = 32 * KW;
   constexpr int HQ = BQ * ROWB, HK = KB * ROWB;  // one 64-column half of a Q / K image
-  constexpr int TILES = 2 * NO;                  // 32x32 dQ tiles of a 64-query tile
+  constexpr int TILES = NQS * NO;                // 32x32 dQ tiles of a query tile
   constexpr int KSPLIT = KW >= TILES ? KW / TILES : 1;
   constexpr int OFF_Q = 0, OFF_DO = OFF_Q + NH * HQ, OFF_K = OFF_DO + NH * HQ;
-  constexpr int OFF_DS = OFF_K + NH * HK, OFF_L = OFF_DS + KB * ROWB;
+  constexpr int OFF_DS = OFF_K + NH * HK, OFF_L = OFF_DS + (BQ / 64) * KB * ROWB;
   constexpr int OFF_MW = OFF_L + 2 * BQ * 4, OFF_P = OFF_MW + KW * BQ * 4;
   constexpr int OFF_PV = OFF_P + (KSPLIT > 1 ? (KSPLIT - 1) * TILES * 64 * 16 * 4 : 0);
+  static_assert(BQ == 64 || (KSPLIT == 1 && !PERSIST), "BQ 128: key-block mode, no split-key dQ");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int w = threadIdx.x >> 6;
   const int BH = a.B * a.H;
@@ -591,7 +598,10 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
 
     uint4 rq[Stager<BQ, NH, NT>::N], rd[Stager<BQ, NH, NT>::N];
     float rl = 0.f;
-    uint32_t rmw = 0xffffffffu;  // no dropout: every key kept
+    constexpr int NMW = KW * BQ / NT;  // keep words staged per thread
+    uint32_t rmw[NMW];
+#pragma unroll
+    for (int i = 0; i < NMW; ++i) rmw[i] = 0xffffffffu;  // no dropout: every key kept
     auto issue = [&](int qt) {
       stq::load(rq, Qg, ld, qt * BQ, a.T, a.hd);
       stq::load(rd, dOg, a.D, qt * BQ, a.T, a.hd);
@@ -600,16 +610,21 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
         const int q = qt * BQ + (t & (BQ - 1));
         rl = q < a.T ? (t < BQ ? -lseg[q] : dlg[q]) : 0.f;  // -lse: the S init (K holds c K)
       }
-      if (a.thr) {  // word j of query row q -> sMW[j * 64 + q]
-        const int q = qt * BQ + (t & 63), j = t >> 6;
-        rmw = (q < a.T && t0w + j < ntw) ? a.dmask[((long)bh * ntw + t0w + j) * a.T + q] : 0u;
+      if (a.thr) {  // word j of query row q -> sMW[j * BQ + q]
+#pragma unroll
+        for (int i = 0; i < NMW; ++i) {
+          const int u = t + NT * i;
+          const int q = qt * BQ + (u & (BQ - 1)), j = u / BQ;
+          rmw[i] = (q < a.T && t0w + j < ntw) ? a.dmask[((long)bh * ntw + t0w + j) * a.T + q] : 0u;
+        }
       }
     };
     auto commit = [&]() {
       stq::store(smem + OFF_Q, rq);
       stq::store(smem + OFF_DO, rd);
       if (threadIdx.x < 2 * BQ) reinterpret_cast<float*>(smem + OFF_L)[threadIdx.x] = rl;
-      reinterpret_cast<uint32_t*>(smem + OFF_MW)[threadIdx.x] = rmw;
+#pragma unroll
+      for (int i = 0; i < NMW; ++i) reinterpret_cast<uint32_t*>(smem + OFF_MW)[threadIdx.x + NT * i] = rmw[i];
     };
     issue(qt0);
     commit();
@@ -660,13 +675,14 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
       const int ta0 = tr_off(4 * h32 + trq, trc), tb0 = tr_off(8 + 4 * h32 + trq, trc);
       const int ta1 = tr_off(4 * h32 + trq, 32 + trc), tb1 = tr_off(8 + 4 * h32 + trq, 32 + trc);
 #pragma unroll
-      for (int qs = 0; qs < 2; ++qs) {
+      for (int qs = 0; qs < NQS; ++qs) {
         const int qsub0 = qbase + qs * 32;
+        char* mydsh = myds + (qs >> 1) * KB * ROWB;  // dS^T half of this subtile's 64 queries
         if (qsub0 + 31 < wave_kmin || wave_kmin >= a.T) {  // every query precedes every key: dS = 0
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            const int qc = qs * 32 + 8 * g + 4 * h32;
-            *reinterpret_cast<uint2*>(myds + lds_off(l32, qc >> 3) + (qc & 7) * 2) = make_uint2(0, 0);
+            const int qc = (qs & 1) * 32 + 8 * g + 4 * h32;
+            *reinterpret_cast<uint2*>(mydsh + lds_off(l32, qc >> 3) + (qc & 7) * 2) = make_uint2(0, 0);
           }
           continue;
         }
@@ -680,7 +696,7 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
           const float4 y = *reinterpret_cast<const float4*>(sL + BQ + q4);
           sacc[4 * g] = x.x; sacc[4 * g + 1] = x.y; sacc[4 * g + 2] = x.z; sacc[4 * g + 3] = x.w;
           dl[4 * g] = y.x; dl[4 * g + 1] = y.y; dl[4 * g + 2] = y.z; dl[4 * g + 3] = y.w;
-          const uint4 m4 = *reinterpret_cast<const uint4*>(sMW + mw_col * 64 + q4);
+          const uint4 m4 = *reinterpret_cast<const uint4*>(sMW + mw_col * BQ + q4);
           mwr[4 * g] = m4.x; mwr[4 * g + 1] = m4.y; mwr[4 * g + 2] = m4.z; mwr[4 * g + 3] = m4.w;
         }
 #pragma unroll
@@ -712,13 +728,13 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
         }
 #pragma unroll
         for (int g = 0; g < 4; ++g) {  // dS^T image row = key, 4 consecutive q per 8-byte write
-          const int qc = qs * 32 + 8 * g + 4 * h32;
-          *reinterpret_cast<uint2*>(myds + lds_off(l32, qc >> 3) + (qc & 7) * 2) =
+          const int qc = (qs & 1) * 32 + 8 * g + 4 * h32;
+          *reinterpret_cast<uint2*>(mydsh + lds_off(l32, qc >> 3) + (qc & 7) * 2) =
               make_uint2(pack2(dp[4 * g], dp[4 * g + 1]), pack2(dp[4 * g + 2], dp[4 * g + 3]));
         }
       }
       __syncthreads();  // dS of all KB keys in LDS
-      // dQ[64 q][hd] = dS[64 q][KB keys] (c K)[KB keys][hd]
+      // dQ[BQ q][hd] = dS[BQ q][KB keys] (c K)[KB keys][hd]
 #pragma unroll
       for (int i = 0; i < NTW; ++i) {
         const int tt = tt0 + i * TSTEP;
@@ -729,9 +745,10 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
         f32x16 dq = {0};
         if (act) {
           // rows klo + 16 kk + 8 h32 + q (+4): the 16 kk part is an immediate
-          const int da = tr_off(8 * h32 + trq, qs * 32 + trc), db = tr_off(8 * h32 + 4 + trq, qs * 32 + trc);
+          const int qcol = (qs & 1) * 32 + trc;
+          const int da = tr_off(8 * h32 + trq, qcol), db = tr_off(8 * h32 + 4 + trq, qcol);
           const int ka = tr_off(8 * h32 + trq, (n & 1) * 32 + trc), kb4 = tr_off(8 * h32 + 4 + trq, (n & 1) * 32 + trc);
-          const char* sdSh = sdS + klo * ROWB;
+          const char* sdSh = sdS + (qs >> 1) * KB * ROWB + klo * ROWB;
           const char* sKh = sK + (n >> 1) * HK + klo * ROWB;
 #pragma unroll
           for (int kk = 0; kk < KSPAN / 16; ++kk)
@@ -880,13 +897,15 @@ __global__ __launch_bounds__(256) void attn_dq_finalize_kernel(const float* __re
   st16_nt(dqkv + (long)r * 3L * D + c, pack8(f));
 }
 
-template <int NKS, int KW>
+template <int NKS, int KW, bool PERSIST>
 constexpr int bwd_smem() {
-  constexpr int NH = (NKS + 3) / 4, NO = (NKS + 1) / 2, KB = 32 * KW, TILES = 2 * NO;
+  constexpr int BQ = bwd_bq<NKS, PERSIST>();
+  constexpr int NH = (NKS + 3) / 4, NO = (NKS + 1) / 2, KB = 32 * KW, TILES = (BQ / 32) * NO;
   constexpr int KSPLIT = KW >= TILES ? KW / TILES : 1;
   constexpr int NTW = KSPLIT > 1 ? 1 : (TILES + KW - 1) / KW;
-  return 2 * NH * BQ * ROWB + NH * KB * ROWB + KB * ROWB + 2 * BQ * 4 + KW * BQ * 4 +
-         (KSPLIT > 1 ? (KSPLIT - 1) * TILES * 64 * 16 * 4 : 0) + (KSPLIT > 1 ? TILES : KW) * NTW * 16 * 64 * 4;
+  return 2 * NH * BQ * ROWB + NH * KB * ROWB + (BQ / 64) * KB * ROWB + 2 * BQ * 4 + KW * BQ * 4 +
+         (KSPLIT > 1 ? (KSPLIT - 1) * TILES * 64 * 16 * 4 : 0) +
+         (PERSIST ? (KSPLIT > 1 ? TILES : KW) * NTW * 16 * 64 * 4 : 0);
 }
 
 int nks_for(int hd);
@@ -924,19 +943,19 @@ bool bwd_persistent(int T, int hd) {
 
 template <int NKS, int KW>
 void launch_bwd(const AttnArgs& a, hipStream_t stream) {
-  constexpr int smem = bwd_smem<NKS, KW>();
-  static_assert(smem <= 160 * 1024, "attention backward LDS budget");
+  constexpr int smem_p = bwd_smem<NKS, KW, true>(), smem_k = bwd_smem<NKS, KW, false>();
+  static_assert(smem_p <= 160 * 1024 && smem_k <= 160 * 1024, "attention backward LDS budget");
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)attn_bwd_kernel<NKS, KW, true>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    hipFuncSetAttribute((const void*)attn_bwd_kernel<NKS, KW, false>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    hipFuncSetAttribute((const void*)attn_bwd_kernel<NKS, KW, true>, hipFuncAttributeMaxDynamicSharedMemorySize, smem_p);
+    hipFuncSetAttribute((const void*)attn_bwd_kernel<NKS, KW, false>, hipFuncAttributeMaxDynamicSharedMemorySize, smem_k);
     attr = true;
   }
   const int nkb = (a.T + 32 * KW - 1) / (32 * KW);
   if (a.dq_part)
-    attn_bwd_kernel<NKS, KW, false><<<a.B * a.H * nkb, 64 * KW, smem, stream>>>(a);
+    attn_bwd_kernel<NKS, KW, false><<<a.B * a.H * nkb, 64 * KW, smem_k, stream>>>(a);
   else
-    attn_bwd_kernel<NKS, KW, true><<<a.B * a.H, 64 * KW, smem, stream>>>(a);
+    attn_bwd_kernel<NKS, KW, true><<<a.B * a.H, 64 * KW, smem_p, stream>>>(a);
 }
 
 int nks_for(int hd) {
