@@ -464,6 +464,26 @@ struct Stager {
       reg[c] = (r < rows && col < hd) ? ld16(base + (long)r * ld + col) : make_uint4(0, 0, 0, 0);
     }
   }
+  // per-thread byte offsets of its chunks from a tile's first row (computed once per kernel)
+  static MG_DEVICE void offsets(uint32_t (&off)[N], long ld) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) {
+      const int idx = threadIdx.x + NT * c;
+      const int rem = idx % (ROWS * 8);
+      off[c] = (uint32_t)(((rem >> 3) * ld + (idx / (ROWS * 8)) * 64 + (rem & 7) * 8) * 2);
+    }
+  }
+  // buffer loads through one descriptor per tile (base = the tile's first row, extent = the rest
+  // of the tensor): no per-lane bounds branches or 64-bit address math per tile.  Rows past the
+  // sequence read the next sequence's (finite) rows, past the tensor zeros; columns past hd read
+  // the neighbouring head.  Callers make both harmless (attn_bwd_kernel: masked rows, zero K / V
+  // columns past hd).
+  static MG_DEVICE void load_buf(uint4 (&reg)[N], const bf16_t* tensor, uint64_t total, uint64_t origin,
+                                 const uint32_t (&off)[N]) {
+    const __amdgpu_buffer_rsrc_t d = kv_rsrc(tensor, total, origin);
+#pragma unroll
+    for (int c = 0; c < N; ++c) reg[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(d, off[c], 0, 0));
+  }
   static MG_DEVICE void store(char* lds, const uint4 (&reg)[N]) {
 #pragma unroll
     for (int c = 0; c < N; ++c) {
@@ -597,14 +617,20 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
     const int qt0 = kb0 / BQ;
 
     uint4 rq[Stager<BQ, NH, NT>::N], rd[Stager<BQ, NH, NT>::N];
+    uint32_t oq[Stager<BQ, NH, NT>::N], od[Stager<BQ, NH, NT>::N];
+    stq::offsets(oq, ld);
+    stq::offsets(od, a.D);
+    const uint64_t q_total = (uint64_t)a.B * a.T * ld * 2, do_total = (uint64_t)a.B * a.T * a.D * 2;
+    const uint64_t q_org = (uint64_t)((const char*)Qg - (const char*)a.qkv);
+    const uint64_t do_org = (uint64_t)((const char*)dOg - (const char*)a.dout);
     float rl = 0.f;
     constexpr int NMW = KW * BQ / NT;  // keep words staged per thread
     uint32_t rmw[NMW];
 #pragma unroll
     for (int i = 0; i < NMW; ++i) rmw[i] = 0xffffffffu;  // no dropout: every key kept
     auto issue = [&](int qt) {
-      stq::load(rq, Qg, ld, qt * BQ, a.T, a.hd);
-      stq::load(rd, dOg, a.D, qt * BQ, a.T, a.hd);
+      stq::load_buf(rq, a.qkv, q_total, q_org + (uint64_t)qt * BQ * ld * 2, oq);
+      stq::load_buf(rd, a.dout, do_total, do_org + (uint64_t)qt * BQ * a.D * 2, od);
       const int t = threadIdx.x;
       if (t < 2 * BQ) {
         const int q = qt * BQ + (t & (BQ - 1));
