@@ -902,7 +902,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const GemmArgs args) {
 // rounds x per-block work, where rounds = ceil(blocks / concurrent slots) and per-block work =
 // its K-tiles + ~2 tiles of prologue/epilogue (the atomic write-back).  A naive "fill the chip"
 // split leaves a mostly idle second round (e.g. 144 tiles x 4 = 576 blocks on 512 slots).
-static int choose_split(int tiles, int slots, int nkt, int ovh, int spmin = 1) {
+static int choose_split(int tiles, int slots, int nkt, int ovh, int spmin = 1, long* cost = nullptr) {
   int best = spmin;
   long bc = -1;
   const int maxsp = std::max(spmin, std::min(32, nkt / 4));
@@ -914,6 +914,7 @@ static int choose_split(int tiles, int slots, int nkt, int ovh, int spmin = 1) {
       best = sp;
     }
   }
+  if (cost) *cost = bc;
   return best;
 }
 
@@ -1224,7 +1225,18 @@ int pick_config(int M, int N, int K, int layout) {
   // shape (bench/dgrad_nn_vs_nt.py, M = 65536: proj 84 / PP 97 us, fc 251 / 290, qkv 182 / 210,
   // fc2 + GELU' 344 / 362), and faster than NT against a transposed weight copy
   if (layout == 1) return t256 >= 256 ? 5 : 1;
-  return (long)M * N >= (1L << 20) ? 5 : 1;  // wgrad: W4 since the asm tr reads (bench_wgrad.py)
+  if ((long)M * N < (1L << 20)) return 1;
+  // wgrad: W4 (256^2 tiles, one block per CU, split-K over 256 slots) unless T128 (128^2, two
+  // blocks per CU, 512 slots) quantises so much better that it pays for its ~15 % lower per-CU
+  // rate.  Both sides through the split-K cost model (rounds x (K-tiles per block + overhead)); a
+  // T128 K-tile is a quarter of the work at 2 blocks per CU and 0.85 of W4's rate: 0.59 W4 K-tiles.
+  // bench_wgrad.py (profiles/round3_streamk_wgrad_ab.txt): gpt2-xl at 16k tokens, qkv 294 vs 366 us
+  // and attention projection 110 vs 130 on T128; every GPT-2 (131k tokens) and LM-head shape on W4.
+  const int nkt = cdiv(K, BK);
+  long c4 = 0, c1 = 0;
+  choose_split((int)t256, 256, nkt, 6, 1, &c4);
+  choose_split(cdiv(M, 128) * cdiv(N, 128), 512, nkt, 3, 1, &c1);
+  return c1 * 59 < c4 * 100 ? 1 : 5;
 }
 
 template <bool AK, bool BKC, int EPI, bool OUTF32>

@@ -91,6 +91,18 @@ def test_tn_acc(Mr, N, K):
     _check(c, ref, Mr)
 
 
+@pytest.mark.parametrize("Mr,N,K", [(8040, 4800, 1704), (16384, 4800, 1600)])
+def test_tn_acc_xl_shapes(Mr, N, K):
+    # gpt2-xl weight-gradient shapes that quantise badly onto 256 CUs as 256^2 tiles (133 tiles: the
+    # auto choice is T128 here, see pick_config); partial M / N tiles and a partial last K-tile
+    # (8040 % 64 = 40) in the first shape
+    a, b = _bf(Mr, N, seed=30, scale=0.5), _bf(Mr, K, seed=31, scale=0.5)
+    c = torch.randn(N, K, device=DEV)
+    ref = c + a.float().t() @ b.float()
+    G.gemm_tn_acc(a, b, c)
+    _check(c, ref, Mr)
+
+
 def test_tn_acc_nvalid():
     Mr, V, ld, K = 128, 1001, 1008, 64
     a, b = _bf(Mr, ld, seed=15), _bf(Mr, K, seed=16)
