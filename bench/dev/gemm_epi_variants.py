@@ -35,7 +35,7 @@ cases = {
     "fc2_dgrad_plain": (lambda: G.gemm_dgrad(dz, wp), 2 * M * 4 * D * D),
     "proj_fwd_resid": (lambda: G.gemm_nt(y, wo, bias=bfc[:D], epi="resid", resid=res, p=0.1, seed=3), 2 * M * D * D),
 }
-for v in [0, 1, 2, 3, 4, 5, 6]:
+for v in [int(x) for x in os.environ.get("VARIANTS", "0,1,2,3,4,5,6").split(",")]:
     C.gemm_set_variant(v)
     row = {}
     for k, (fn, fl) in cases.items():
@@ -44,5 +44,5 @@ for v in [0, 1, 2, 3, 4, 5, 6]:
             row[k] = [round(t * 1e3, 1), round(fl / t / 1e9)]
         except Exception as ex:  # noqa: BLE001
             row[k] = str(ex)[:60]
-    print(json.dumps({"variant": v, "us_tflops": row}), flush=True)
+    print(json.dumps({"variant": v, "stagger": os.environ.get("MINGPT_GEMM_STAGGER"), "us_tflops": row}), flush=True)
 C.gemm_set_variant(0)

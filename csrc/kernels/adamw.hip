@@ -47,6 +47,15 @@ __global__ __launch_bounds__(256) void sumsq_final_kernel(const float* __restric
   }
 }
 
+typedef float f32v4 __attribute__((ext_vector_type(4)));
+MG_DEVICE void ld4_nt(const float* p, float (&o)[4]) {
+  const f32v4 v = __builtin_nontemporal_load(reinterpret_cast<const f32v4*>(p));
+  o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+}
+MG_DEVICE void st4_nt(float* p, const float (&a)[4]) {
+  __builtin_nontemporal_store(f32v4{a[0], a[1], a[2], a[3]}, reinterpret_cast<f32v4*>(p));
+}
+
 // Gradient loads: fp32 main grads, or the bf16 buffer a bf16 all-reduce / reduce-scatter left.
 MG_DEVICE void load_grad4(const float* g, long e, float (&o)[4]) {
   const float4 v = *reinterpret_cast<const float4*>(g + e);
@@ -115,26 +124,52 @@ __global__ __launch_bounds__(256) void adamw_kernel(
   }
   const float decay = 1.f - lr * wd;
   const float step = lr / bc1;
-  for (int i = threadIdx.x * 4; i < len; i += 256 * 4) {
+  // every operand is touched once per step: non-temporal loads / stores (no L2 / MALL pollution),
+  // and two float4 groups per thread per iteration so 8 loads are in flight before any use
+  auto upd = [&](float (&pa)[4], const float (&ga)[4], float (&ma)[4], float (&va)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gg = ga[j] * gs;
+      ma[j] = b1 * ma[j] + (1.f - b1) * gg;
+      va[j] = b2 * va[j] + (1.f - b2) * gg * gg;
+      pa[j] = pa[j] * decay - step * ma[j] / (sqrtf(va[j]) / bc2_sqrt + eps);
+    }
+  };
+  int i = threadIdx.x * 4;
+  for (; i + 1024 + 4 <= len; i += 2048) {
+    float pa[2][4], ga[2][4], ma[2][4], va[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long e = s0 + i + u * 1024, me = ms0 + i + u * 1024;
+      ld4_nt(master + e, pa[u]);
+      load_grad4(grad, e, ga[u]);
+      ld4_nt(m + me, ma[u]);
+      ld4_nt(v + me, va[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long e = s0 + i + u * 1024, me = ms0 + i + u * 1024;
+      upd(pa[u], ga[u], ma[u], va[u]);
+      st4_nt(master + e, pa[u]);
+      st4_nt(m + me, ma[u]);
+      st4_nt(v + me, va[u]);
+      typedef unsigned v2u __attribute__((ext_vector_type(2)));
+      __builtin_nontemporal_store(v2u{pack2(pa[u][0], pa[u][1]), pack2(pa[u][2], pa[u][3])},
+                                  reinterpret_cast<v2u*>(param + e));
+    }
+  }
+  for (; i < len; i += 1024) {
     const long e = s0 + i, me = ms0 + i;
     if (i + 4 <= len) {
-      float4 p = *reinterpret_cast<float4*>(master + e);
-      float ga[4];
+      float pa[4], ga[4], ma[4], va[4];
+      ld4_nt(master + e, pa);
       load_grad4(grad, e, ga);
-      float4 mm = *reinterpret_cast<float4*>(m + me);
-      float4 vv = *reinterpret_cast<float4*>(v + me);
-      float pa[4] = {p.x, p.y, p.z, p.w};
-      float ma[4] = {mm.x, mm.y, mm.z, mm.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float gg = ga[j] * gs;
-        ma[j] = b1 * ma[j] + (1.f - b1) * gg;
-        va[j] = b2 * va[j] + (1.f - b2) * gg * gg;
-        pa[j] = pa[j] * decay - step * ma[j] / (sqrtf(va[j]) / bc2_sqrt + eps);
-      }
-      *reinterpret_cast<float4*>(master + e) = make_float4(pa[0], pa[1], pa[2], pa[3]);
-      *reinterpret_cast<float4*>(m + me) = make_float4(ma[0], ma[1], ma[2], ma[3]);
-      *reinterpret_cast<float4*>(v + me) = make_float4(va[0], va[1], va[2], va[3]);
+      ld4_nt(m + me, ma);
+      ld4_nt(v + me, va);
+      upd(pa, ga, ma, va);
+      st4_nt(master + e, pa);
+      st4_nt(m + me, ma);
+      st4_nt(v + me, va);
       *reinterpret_cast<uint2*>(param + e) = make_uint2(pack2(pa[0], pa[1]), pack2(pa[2], pa[3]));
     } else {
       for (int j = 0; j < 4 && i + j < len; ++j) {

@@ -26,6 +26,11 @@ timeout -k 10 400 python bench.py --steps 10 --warmup 3 > "$OUT/bench.json" 2> "
 cat "$OUT/bench.json"
 timeout -k 10 300 python bench.py --steps 5 --warmup 2 --also-batch 0 --comm-at-world1 > "$OUT/bench_comm1.json" 2> "$OUT/bench_comm1.err" || { tail -20 "$OUT/bench_comm1.err"; exit 1; }
 cat "$OUT/bench_comm1.json"
+if [ -x build/bin/xgmi_probe ]; then
+  timeout -k 10 120 build/bin/xgmi_probe --max-mb 256 > "$OUT/xgmi_probe.txt" 2>&1 || { tail -20 "$OUT/xgmi_probe.txt"; exit 1; }
+  python -c "import torch; print('torch.cuda.nccl.version():', torch.cuda.nccl.version())" >> "$OUT/xgmi_probe.txt" 2>/dev/null
+  head -3 "$OUT/xgmi_probe.txt"
+fi
 if [ $PROF = 1 ]; then
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
     python3 bench.py --steps 5 --warmup 2 --also-batch 0 > "$OUT/prof_bench.log" 2>&1 || { tail -20 "$OUT/prof_bench.log"; exit 1; }
