@@ -34,7 +34,13 @@ cases = {
     "fc2_dgrad_gelu": (lambda: G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=gd), 2 * M * 4 * D * D),
     "fc2_dgrad_plain": (lambda: G.gemm_dgrad(dz, wp), 2 * M * 4 * D * D),
     "proj_fwd_resid": (lambda: G.gemm_nt(y, wo, bias=bfc[:D], epi="resid", resid=res, p=0.1, seed=3), 2 * M * D * D),
+    "qkv_fwd_bias": (lambda: G.gemm_nt(x, wfc[:3 * D], bias=bfc[:3 * D], epi="bias"), 2 * M * 3 * D * D),
 }
+if os.environ.get("LMHEAD"):
+    wte = r(50304, D)
+    cases["lmhead_fwd"] = (lambda: G.gemm_nt(x, wte), 2 * M * 50304 * D)
+if os.environ.get("CASES"):
+    cases = {k: v for k, v in cases.items() if k in os.environ["CASES"].split(",")}
 for v in [int(x) for x in os.environ.get("VARIANTS", "0,1,2,3,4,5,6").split(",")]:
     C.gemm_set_variant(v)
     row = {}

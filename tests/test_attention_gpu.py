@@ -9,10 +9,12 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.fixture(autouse=True, params=[1, 2], ids=["bwd_persistent", "bwd_partials"])
+@pytest.fixture(autouse=True, params=[1, 2, 3], ids=["bwd_persistent", "bwd_partials", "bwd4"])
 def bwd_mode(request):
-    """Every test under both backward schedules: one workgroup per (b, h) summing dQ in place,
-    and one workgroup per (key block, b, h) with dQ partials + a finalize pass."""
+    """Every test under the backward schedules: one workgroup per (b, h) summing dQ in place, one
+    workgroup per (key block, b, h) with dQ partials + a finalize pass (8 waves x 32 keys), and the
+    one-wave-per-SIMD key-block kernel (4 waves x 64 keys; hd = 64 and T a multiple of 256 > 256,
+    else the 8-wave key-block kernel)."""
     ext().attention_set_bwd_mode(request.param)
     yield request.param
     ext().attention_set_bwd_mode(0)
@@ -176,7 +178,7 @@ def test_attention_fwd_head_dims(hd):
         torch.testing.assert_close(lse.view(B, H, T), lse_ref, atol=2e-2, rtol=1e-3)
 
 
-@pytest.mark.parametrize("T", [128, 320])
+@pytest.mark.parametrize("T", [128, 320, 512, 1024])
 def test_attention_dropout_exact(T):
     """Forward and backward with dropout vs an fp32 reference that uses the kernel's exact mask."""
     C = ext()
