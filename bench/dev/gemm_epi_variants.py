@@ -50,5 +50,5 @@ for v in [int(x) for x in os.environ.get("VARIANTS", "0,1,2,3,4,5,6").split(",")
             row[k] = [round(t * 1e3, 1), round(fl / t / 1e9)]
         except Exception as ex:  # noqa: BLE001
             row[k] = str(ex)[:60]
-    print(json.dumps({"variant": v, "stagger": os.environ.get("MINGPT_GEMM_STAGGER"), "us_tflops": row}), flush=True)
+    print(json.dumps({"variant": v, "us_tflops": row}), flush=True)
 C.gemm_set_variant(0)

@@ -84,7 +84,6 @@ struct GemmArgs {
   int dT, dH, dhd;            // EPI 5: sequence length, heads, head dim (hd in {8, 16, 32, 64})
   long drow0;                 // EPI 5: global row of this launch's row 0 (row-chunked launches)
   int nt_out;                 // non-temporal bf16 output stores (see gemm() below)
-  int stagger;                // W4: first-round blocks of CU group g sleep g * stagger * 1024 cycles
 };
 
 static unsigned long long* g_dbg = nullptr;  // MG_GEMM_STAMPS builds: stamp buffer
@@ -1043,10 +1042,6 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
 #define W4_KSTAMP(k)
 #endif
   W4_STAMP(6);
-  if (args.stagger && orig < 256) {  // de-phase the CUs' epilogue store bursts (experiment)
-    const int g = (orig >> 3) & 3;
-    for (int i = 0; i < g * args.stagger; ++i) __builtin_amdgcn_s_sleep(16);
-  }
   f32x4 acc[8][FN];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -1292,9 +1287,6 @@ void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long l
     static int nt = -1;
     if (nt < 0) { const char* e = getenv("MINGPT_GEMM_NT_STORE"); nt = e ? atoi(e) : 1; }
     a.nt_out = nt != 0;
-    static int stg = -1;
-    if (stg < 0) { const char* e = getenv("MINGPT_GEMM_STAGGER"); stg = e ? atoi(e) : 0; }
-    a.stagger = stg;
   }
   if (layout == 0) {
     if (epi == 0) dispatch<true, true, 0, false>(a, stream);
