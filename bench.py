@@ -89,8 +89,11 @@ def _comm_diag(eng, info, N, comm_ms):
            "comm_exposed_ms": None if comm_ms is None else round(comm_ms, 3)}
     if eng.dp is not None:
         out.update(eng.dp.comm_plan())
+        if eng.dp.native is not None:
+            out["rccl_version_native"] = eng.dp.native.version_str
     else:
-        out.update({"n_buckets": None, "bucket_bytes": None, "wire_dtype": None, "collective": None})
+        out.update({"n_buckets": None, "bucket_bytes": None, "wire_dtype": None, "collective": None,
+                    "comm_backend": None})
     return out
 
 
@@ -119,6 +122,9 @@ def main():
                     help="second timed pass at this per-GPU batch (0: skip), reported under 'extra'")
     ap.add_argument("--comm-at-world1", action="store_true",
                     help="N = 1: drive the RCCL collective path on a one-rank group (plumbing check)")
+    ap.add_argument("--comm", default=None, choices=["c10d", "rccl"],
+                    help="gradient communicator: c10d's RCCL process group (default, or MINGPT_COMM) "
+                         "or the engine's own RCCL communicator + comm stream (parallel/comm.py)")
     a = ap.parse_args()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_launch_ranks(a.gpus))  # parent: no GPU call happens in this process
@@ -143,7 +149,7 @@ def main():
     eng = StepEngine(model, lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, grad_clip=1.0,
                      bucket_mb=a.bucket_mb, zero1=a.zero1,
                      reduce_dtype=torch.bfloat16 if a.reduce_dtype == "bf16" else None,
-                     comm_at_world1=a.comm_at_world1)
+                     comm_at_world1=a.comm_at_world1, comm=a.comm)
     g = torch.Generator(device=eng.device).manual_seed(99 + info.rank)
     step = (lambda x, y: eng.graph_step(x, y)) if a.graph else (lambda x, y: eng.train_step([(x, y)]))
 

@@ -4,6 +4,8 @@
 Explicit ``hipcc --offload-arch=gfx950`` compiles (no hipify pass, no JIT cache):
 
 * each ``csrc/kernels/*.hip`` -> object with device code for gfx950 only,
+* ``csrc/comm/*.cpp``         -> the native RCCL communicator (no link-time RCCL: it binds the
+  RCCL torch already loaded, see csrc/comm/rccl_comm.cpp),
 * ``csrc/bindings.cpp``       -> host object against the torch headers,
 * link against the HIP runtime *bundled with torch* (``torch/lib/libamdhip64.so``), so the
   process holds exactly one HIP runtime and our kernels share torch's streams and allocator.
@@ -67,6 +69,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True, debug: bool 
     os.makedirs(bdir, exist_ok=True)
     headers = glob.glob(os.path.join(ROOT, "csrc", "include", "*.h"))
     kernels = sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip")))
+    kernels += sorted(glob.glob(os.path.join(ROOT, "csrc", "comm", "*.cpp")))  # host code (HIP runtime + RCCL)
     incs, tlib, abi = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
 

@@ -5,6 +5,7 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
+#include "comm.h"
 #include "kernels.h"
 
 namespace {
@@ -565,9 +566,80 @@ at::Tensor attention_decode(const at::Tensor& qkv_new, const at::Tensor& cache, 
   return out;
 }
 
+// ------------------------------------------------------------------------------- native RCCL
+// csrc/comm/rccl_comm.cpp.  Every collective runs on the communicator's comm stream after the
+// tensor's device's CURRENT stream (the producers); comm_wait makes that stream wait again.
+mg::comm::DType comm_dtype(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return mg::comm::DType::F32;
+    case at::kBFloat16: return mg::comm::DType::BF16;
+    case at::kHalf: return mg::comm::DType::F16;
+    case at::kLong: return mg::comm::DType::I64;
+    case at::kByte: return mg::comm::DType::U8;
+    default: TORCH_CHECK(false, "comm: unsupported dtype ", t.scalar_type());
+  }
+}
+
+hipStream_t comm_cs(int64_t h, const at::Tensor& t) {
+  CHECK_DEV(t);
+  CHECK_CONTIG(t);
+  TORCH_CHECK(t.device().index() == mg::comm::device(h), "comm: tensor on device ", t.device().index(),
+              ", communicator on device ", mg::comm::device(h));
+  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
+}
+
+int64_t comm_all_reduce(int64_t h, const at::Tensor& t) {
+  hipStream_t cs = comm_cs(h, t);
+  return mg::comm::all_reduce(h, t.data_ptr(), (size_t)t.numel(), comm_dtype(t), cs);
+}
+
+int64_t comm_reduce_scatter(int64_t h, const at::Tensor& in, const at::Tensor& out) {
+  hipStream_t cs = comm_cs(h, in);
+  comm_cs(h, out);
+  TORCH_CHECK(in.scalar_type() == out.scalar_type(), "comm_reduce_scatter: dtype mismatch");
+  TORCH_CHECK(in.numel() == out.numel() * mg::comm::nranks(h), "comm_reduce_scatter: input must hold nranks x output");
+  return mg::comm::reduce_scatter(h, in.data_ptr(), out.data_ptr(), (size_t)out.numel(), comm_dtype(in), cs);
+}
+
+int64_t comm_all_gather(int64_t h, const at::Tensor& in, const at::Tensor& out) {
+  hipStream_t cs = comm_cs(h, in);
+  comm_cs(h, out);
+  TORCH_CHECK(in.scalar_type() == out.scalar_type(), "comm_all_gather: dtype mismatch");
+  TORCH_CHECK(out.numel() == in.numel() * mg::comm::nranks(h), "comm_all_gather: output must hold nranks x input");
+  return mg::comm::all_gather(h, in.data_ptr(), out.data_ptr(), (size_t)in.numel(), comm_dtype(in), cs);
+}
+
+int64_t comm_broadcast(int64_t h, const at::Tensor& t, int64_t root) {
+  hipStream_t cs = comm_cs(h, t);
+  TORCH_CHECK(root >= 0 && root < mg::comm::nranks(h), "comm_broadcast: bad root");
+  return mg::comm::broadcast(h, t.data_ptr(), (size_t)t.numel(), comm_dtype(t), (int)root, cs);
+}
+
+void comm_wait(int64_t h, int64_t ticket) {
+  const int d = mg::comm::device(h);
+  mg::comm::wait(h, ticket, c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(d).stream());
+}
+
 }  // namespace
 
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("comm_load", [](const std::string& path) {
+    mg::comm::load_rccl(path);
+    return (int64_t)mg::comm::rccl_version();
+  }, py::arg("path") = std::string());
+  m.def("comm_unique_id", []() { return py::bytes(mg::comm::unique_id()); });
+  m.def("comm_create", [](const py::bytes& uid, int64_t nranks, int64_t rank, int64_t device) {
+    return mg::comm::create(std::string(uid), (int)nranks, (int)rank, (int)device);
+  });
+  m.def("comm_destroy", &mg::comm::destroy);
+  m.def("comm_stream_ptr", [](int64_t h) { return (int64_t)(intptr_t)mg::comm::comm_stream(h); });
+  m.def("comm_all_reduce", &comm_all_reduce);
+  m.def("comm_reduce_scatter", &comm_reduce_scatter);
+  m.def("comm_all_gather", &comm_all_gather);
+  m.def("comm_broadcast", &comm_broadcast);
+  m.def("comm_wait", &comm_wait);
+  m.def("comm_pending", &mg::comm::pending);
   m.doc() = "mingpt_distributed_amd gfx950 kernels";
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);

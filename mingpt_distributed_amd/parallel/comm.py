@@ -1,0 +1,123 @@
+"""Native RCCL communicator for the data-parallel engines (``csrc/comm/rccl_comm.cpp``).
+
+The reference's gradient traffic goes through c10d ``ProcessGroupNCCL`` inside DDP
+(``/root/reference/mingpt/train.py:34``, ``trainer.py:71``).  With ``comm="rccl"`` (or
+``MINGPT_COMM=rccl``) :class:`~.ddp.DataParallelEngine` and :class:`~.zero.ZeroGradEngine` drive
+RCCL themselves instead:
+
+* **Bootstrap** over the existing process group: rank 0's ``ncclGetUniqueId`` bytes are broadcast
+  (``broadcast_object_list``), then every rank calls ``ncclCommInitRank`` on its GPU.  The RCCL is
+  the one torch already loaded (``torch/lib/librccl.so``, soname ``librccl.so.1``), bound by
+  ``dlopen(RTLD_NOLOAD)`` -- never a second RCCL from ``/opt/rocm``.
+* **One comm stream** (highest HIP priority) per communicator.  A collective first makes the comm
+  stream wait for everything the caller's current stream has enqueued (the bucket's producers:
+  an event, no host sync), and returns a :class:`Work` whose ``wait()`` makes the current stream
+  wait for the collective's completion event -- the same contract as c10d's
+  ``async_op=True`` work on RCCL, without c10d's per-call bookkeeping, watchdog or work objects.
+* Sums only (gradients); in-place all-reduce, reduce-scatter into the caller's own slice of the
+  bucket, all-gather out of it, broadcast.
+
+c10d stays the default: the native path is exercised on one GPU (a one-rank communicator,
+``tests/test_comm_gpu.py``) but not yet measured across GPUs.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+def _torch_rccl_path() -> str:
+    return os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+
+
+def comm_backend_default() -> str:
+    """``MINGPT_COMM``: ``c10d`` (default) or ``rccl`` (this module)."""
+    v = os.environ.get("MINGPT_COMM", "c10d").lower()
+    if v not in ("c10d", "rccl"):
+        raise ValueError(f"MINGPT_COMM must be c10d or rccl, not {v!r}")
+    return v
+
+
+class Work:
+    """One collective in flight: ``wait()`` orders the caller's current stream after it."""
+
+    __slots__ = ("_comm", "_ticket")
+
+    def __init__(self, comm: "RcclCommunicator", ticket: int):
+        self._comm, self._ticket = comm, ticket
+
+    def wait(self):
+        if self._ticket is not None:
+            self._comm._C.comm_wait(self._comm.handle, self._ticket)
+            self._ticket = None
+
+    def is_completed(self) -> bool:
+        return self._ticket is None
+
+
+class RcclCommunicator:
+    """An RCCL communicator over the ranks of ``process_group`` on ``device`` (see module doc)."""
+
+    def __init__(self, process_group=None, device: Optional[torch.device] = None):
+        from ..ops._ext import ext
+
+        if not dist.is_initialized():
+            raise RuntimeError("RcclCommunicator: initialise torch.distributed first (bootstrap store)")
+        device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        if device.type != "cuda":
+            raise RuntimeError("RcclCommunicator: a GPU device is required (RCCL)")
+        self._C = ext()
+        self.version = int(self._C.comm_load(_torch_rccl_path()))
+        self.pg = process_group
+        self.rank = dist.get_rank(process_group)
+        self.world = dist.get_world_size(process_group)
+        self.device = device
+        box = [self._C.comm_unique_id() if self.rank == 0 else None]
+        src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
+        dist.broadcast_object_list(box, src=src, group=process_group)
+        with torch.cuda.device(device):
+            self.handle = int(self._C.comm_create(box[0], self.world, self.rank, device.index))
+        self.stream = torch.cuda.ExternalStream(int(self._C.comm_stream_ptr(self.handle)), device=device)
+
+    @property
+    def version_str(self) -> str:
+        v = self.version
+        return f"{v // 10000}.{(v // 100) % 100}.{v % 100}"
+
+    def _tensor(self, t: torch.Tensor) -> torch.Tensor:
+        t.record_stream(self.stream)  # the comm stream uses it: keep the allocator from reusing it early
+        return t
+
+    def all_reduce(self, t: torch.Tensor) -> Work:
+        """In-place sum over ranks."""
+        return Work(self, int(self._C.comm_all_reduce(self.handle, self._tensor(t))))
+
+    def reduce_scatter(self, inp: torch.Tensor, out: torch.Tensor) -> Work:
+        """``out`` (numel = inp.numel() / world) <- this rank's slice of the sum of ``inp`` over
+        ranks; ``out`` may be that slice of ``inp`` itself (in place)."""
+        return Work(self, int(self._C.comm_reduce_scatter(self.handle, self._tensor(inp), self._tensor(out))))
+
+    def all_gather(self, inp: torch.Tensor, out: torch.Tensor) -> Work:
+        """``out`` (numel = world x inp.numel()) <- every rank's ``inp`` in rank order; ``inp``
+        may be this rank's slice of ``out`` (in place)."""
+        return Work(self, int(self._C.comm_all_gather(self.handle, self._tensor(inp), self._tensor(out))))
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> Work:
+        return Work(self, int(self._C.comm_broadcast(self.handle, self._tensor(t), int(src))))
+
+    def pending(self) -> int:
+        return int(self._C.comm_pending(self.handle))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self._C.comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass

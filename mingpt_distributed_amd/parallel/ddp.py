@@ -33,6 +33,9 @@ for one node of 8 MI355X on a point-to-point xGMI mesh:
   backward is exactly that one reduction.
 * The average over ranks (1/world) is folded into the optimizer's grad scale; the constant
   causal mask is never broadcast (there is no mask buffer; fixes D30).
+* **Communicator**: c10d's RCCL process group by default, or (``comm="rccl"`` /
+  ``MINGPT_COMM=rccl``) the engine's own RCCL communicator and comm stream
+  (:mod:`.comm`, ``csrc/comm/rccl_comm.cpp``) with the same stream-ordered wait contract.
 """
 from __future__ import annotations
 
@@ -66,9 +69,12 @@ def _to_bf16(src: torch.Tensor, dst: torch.Tensor):
 class DataParallelEngine:
     def __init__(self, store: FlatParamStore, process_group=None, bucket_mb: float = 32.0,
                  reduce_dtype: Optional[torch.dtype] = None, broadcast: bool = True,
-                 comm_at_world1: bool = False):
+                 comm_at_world1: bool = False, comm: Optional[str] = None, native=None):
         """``comm_at_world1`` runs the collective path even in a one-rank process group (tests
-        of the RCCL calls on a one-GPU box); otherwise one rank means no communication."""
+        of the RCCL calls on a one-GPU box); otherwise one rank means no communication.
+        ``comm``: ``"c10d"`` or ``"rccl"`` (native communicator; default ``MINGPT_COMM``), GPU
+        stores only; ``native``: an existing :class:`~.comm.RcclCommunicator` to reuse (rebuilt
+        engines after a bucket relayout)."""
         self.store = store
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
@@ -90,6 +96,14 @@ class DataParallelEngine:
         self.comm = None  # bf16 reduce buffer (same layout as store.grad)
         self.observed: Optional[List[int]] = None  # ready order of the first synchronised backward
         self._recording: Optional[List[int]] = []
+        from .comm import RcclCommunicator, comm_backend_default
+
+        self.comm_backend = comm or comm_backend_default()
+        self.native = None
+        if self.active and self.comm_backend == "rccl":
+            if store.device.type != "cuda":
+                raise RuntimeError("comm='rccl' needs GPU parameters (RCCL); use c10d for CPU runs")
+            self.native = native if native is not None else RcclCommunicator(process_group, store.device)
         if self.active:
             if self.reduce_dtype is not None:
                 self.comm = torch.empty(store.total, dtype=self.reduce_dtype, device=store.device)
@@ -111,7 +125,10 @@ class DataParallelEngine:
     # ------------------------------------------------------------------ setup
     def broadcast_params(self, src: int = 0):
         """Make rank ``src``'s weights authoritative (DDP ctor broadcast, C3)."""
-        dist.broadcast(self.store.master, src, group=self.pg)
+        if self.native is not None:
+            self.native.broadcast(self.store.master, src).wait()
+        else:
+            dist.broadcast(self.store.master, src, group=self.pg)
         self.store.sync_params_from_master()
 
     @property
@@ -166,7 +183,10 @@ class DataParallelEngine:
         return out
 
     def _launch(self, b: _Bucket):
-        b.work = dist.all_reduce(self._wire(b), op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        if self.native is not None:
+            b.work = self.native.all_reduce(self._wire(b))
+        else:
+            b.work = dist.all_reduce(self._wire(b), op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     # ------------------------------------------------------------------ step boundary
     def _wait_all(self):
@@ -231,7 +251,8 @@ class DataParallelEngine:
         return {"n_buckets": len(self.buckets),
                 "bucket_bytes": [(b.end - b.start) * esz for b in self.buckets],
                 "wire_dtype": "bf16" if esz == 2 else "fp32",
-                "collective": self.collective_kind}
+                "collective": self.collective_kind,
+                "comm_backend": "rccl-native" if self.native is not None else "c10d"}
 
     collective_kind = "all_reduce"
 

@@ -51,9 +51,9 @@ class ZeroGradEngine(DataParallelEngine):
 
     def __init__(self, store: FlatParamStore, process_group=None, broadcast: bool = True,
                  reduce_dtype: Optional[torch.dtype] = None, model: Optional[torch.nn.Module] = None,
-                 comm_at_world1: bool = False):
+                 comm_at_world1: bool = False, comm: Optional[str] = None, native=None):
         super().__init__(store, process_group, reduce_dtype=reduce_dtype, broadcast=broadcast,
-                         comm_at_world1=comm_at_world1)
+                         comm_at_world1=comm_at_world1, comm=comm, native=native)
         multi = self.active
         self.rank = dist.get_rank(process_group) if multi else 0
         for s, e, _ in store.buckets:
@@ -92,6 +92,9 @@ class ZeroGradEngine(DataParallelEngine):
         bi = self.buckets.index(b)
         lo, hi = self.own[bi]
         out = wire[lo - b.start:hi - b.start]
+        if self.native is not None:
+            b.work = self.native.reduce_scatter(wire, out)
+            return
         b.work = dist.reduce_scatter_tensor(out, wire, op=dist.ReduceOp.SUM, group=self.pg,
                                             async_op=True)
 
@@ -116,6 +119,8 @@ class ZeroGradEngine(DataParallelEngine):
                 shard = flat[lo:hi].clone()
                 self.gather_work[bi] = dist.all_gather(list(full.chunk(self.world)), shard,
                                                        group=self.pg, async_op=True)
+            elif self.native is not None:
+                self.gather_work[bi] = self.native.all_gather(flat[lo:hi], full)
             else:
                 self.gather_work[bi] = dist.all_gather_into_tensor(full, flat[lo:hi], group=self.pg,
                                                                    async_op=True)
@@ -148,6 +153,8 @@ class ZeroGradEngine(DataParallelEngine):
             full = buf[b.start:b.end]
             if self._gloo:
                 dist.all_gather(list(full.chunk(self.world)), buf[lo:hi].clone(), group=self.pg)
+            elif self.native is not None:
+                self.native.all_gather(buf[lo:hi], full).wait()
             else:
                 dist.all_gather_into_tensor(full, buf[lo:hi], group=self.pg)
 

@@ -53,10 +53,12 @@ class StepEngine:
     def __init__(self, model: torch.nn.Module, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
                  weight_decay: float = 0.1, grad_clip: float = 1.0, decay_names=None,
                  device: Optional[torch.device] = None, bucket_mb: float = 32.0, reduce_dtype=None,
-                 zero1: bool = False, comm_at_world1: bool = False):
+                 zero1: bool = False, comm_at_world1: bool = False, comm: Optional[str] = None):
         """``reduce_dtype``: None (fp32 gradients on the wire) or ``torch.bfloat16``.
         ``zero1``: shard the AdamW state over the data-parallel ranks (also valid at world 1).
-        ``comm_at_world1``: drive the collectives even in a one-rank process group (tests)."""
+        ``comm_at_world1``: drive the collectives even in a one-rank process group (tests).
+        ``comm``: ``c10d`` or ``rccl`` (the engines' own RCCL communicator, parallel/comm.py);
+        default ``MINGPT_COMM`` or c10d."""
         if device is None:
             info = D.info()
             if info.device.type == "cuda":
@@ -74,6 +76,7 @@ class StepEngine:
         multi = D.is_initialized() and (torch.distributed.get_world_size() > 1 or comm_at_world1)
         world = torch.distributed.get_world_size() if multi else 1
         self.comm_at_world1 = comm_at_world1
+        self.comm = comm
         if reduce_dtype == "auto":
             reduce_dtype = None
         self.zero1 = bool(zero1)
@@ -87,13 +90,13 @@ class StepEngine:
             self.store = FlatParamStore(model, device=self.device, bucket_numel=bucket_numel,
                                         bucket_align=64 * world)
             self.dp = ZeroGradEngine(self.store, reduce_dtype=reduce_dtype, model=model,
-                                     comm_at_world1=comm_at_world1)
+                                     comm_at_world1=comm_at_world1, comm=comm)
             self.opt = ZeroAdamW(self.store, self.dp, **self._okw)
         else:
             self.store = FlatParamStore(model, device=self.device, bucket_numel=bucket_numel)
             self.opt = FusedAdamW(self.store, **self._okw)
             self.dp = DataParallelEngine(self.store, bucket_mb=bucket_mb, reduce_dtype=reduce_dtype,
-                                         comm_at_world1=comm_at_world1) if multi else None
+                                         comm_at_world1=comm_at_world1, comm=comm) if multi else None
             if self.dp is not None:
                 self.opt.grad_buffer = self.dp.grad_buffer
         self.world = self.dp.world if self.dp else 1
@@ -132,8 +135,10 @@ class StepEngine:
         old_store.master = old_store.flat = None  # copied into `new`; only its layout is read below
         self.opt.rehome(new)
         self.store = new
+        native = self.dp.native if self.dp is not None else None  # the communicator outlives the layout
         self.dp = DataParallelEngine(new, bucket_mb=self.bucket_mb, reduce_dtype=self.reduce_dtype,
-                                     broadcast=False, comm_at_world1=self.comm_at_world1)
+                                     broadcast=False, comm_at_world1=self.comm_at_world1, comm=self.comm,
+                                     native=native)
         self.dp.observed = None
         self.dp._recording = None
         self.opt.grad_buffer = self.dp.grad_buffer

@@ -207,3 +207,46 @@ trainer_config: {{max_epochs: 1, batch_size: 8, grad_norm_clip: 1.0, snapshot_pa
     assert "Resuming training from epoch 0 step 5" in out
     snap = torch.load(str(tmp_path / "s.pt"), weights_only=True)
     assert snap["step"] == 12 and snap["final_epoch"] == 0 and snap["epoch_step"] == 0
+
+
+def _worker_comm_cpu(port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from mingpt_distributed_amd.optim import FlatParamStore
+    from mingpt_distributed_amd.parallel.ddp import DataParallelEngine
+
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    store = FlatParamStore(torch.nn.Linear(4, 4), device=torch.device("cpu"), bucket_numel=64)
+    msgs = []
+    try:
+        DataParallelEngine(store, comm_at_world1=True, comm="rccl")
+    except RuntimeError as e:
+        msgs.append(str(e))
+    eng = DataParallelEngine(store, comm_at_world1=True, comm="c10d")
+    msgs.append(eng.comm_plan()["comm_backend"])
+    dist.destroy_process_group()
+    with open(os.path.join(out_dir, "msgs.txt"), "w") as f:
+        f.write("\n".join(msgs))
+
+
+def test_comm_backend_selection_cpu(tmp_path, monkeypatch):
+    """The native RCCL communicator is GPU-only and says so on a CPU store; MINGPT_COMM is
+    validated; c10d stays the default and is what comm_plan() reports."""
+    from mingpt_distributed_amd.parallel.comm import comm_backend_default
+
+    monkeypatch.delenv("MINGPT_COMM", raising=False)
+    assert comm_backend_default() == "c10d"
+    monkeypatch.setenv("MINGPT_COMM", "RCCL")
+    assert comm_backend_default() == "rccl"
+    monkeypatch.setenv("MINGPT_COMM", "mpi")
+    with pytest.raises(ValueError):
+        comm_backend_default()
+    monkeypatch.delenv("MINGPT_COMM")
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_worker_comm_cpu, args=(_port(), str(tmp_path)))
+    p.start()
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    msgs = (tmp_path / "msgs.txt").read_text().splitlines()
+    assert "GPU" in msgs[0] and msgs[1] == "c10d"

@@ -177,9 +177,10 @@ def test_gpu_zero1_matches_replicated(tmp_path):
 
 
 # ------------------------------------------------------------------------------ RCCL paths
-def _worker_rccl1(port, out_dir, zero1, bf16):
+def _worker_rccl1(port, out_dir, zero1, bf16, comm="c10d"):
     """One rank on a real ``nccl`` (RCCL) process group with the collective path forced on:
-    the bucket all-reduce / in-place reduce-scatter and all-gather calls run on RCCL."""
+    the bucket all-reduce / in-place reduce-scatter and all-gather calls run on RCCL (through
+    c10d, or through the engine's own communicator with ``comm="rccl"``)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
 
@@ -189,8 +190,9 @@ def _worker_rccl1(port, out_dir, zero1, bf16):
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     eng = StepEngine(_model(), lr=1e-3, grad_clip=1.0, device=dev, bucket_mb=0.5, zero1=zero1,
-                     reduce_dtype=torch.bfloat16 if bf16 else None, comm_at_world1=True)
+                     reduce_dtype=torch.bfloat16 if bf16 else None, comm_at_world1=True, comm=comm)
     assert eng.dp is not None and eng.dp.active and len(eng.dp.buckets) > 3
+    assert (eng.dp.native is not None) == (comm == "rccl")
     x, y = _batch()
     eng.measure_comm = True  # bench.py's comm_exposed_ms plumbing on the real RCCL path
     for _ in range(3):
@@ -200,6 +202,11 @@ def _worker_rccl1(port, out_dir, zero1, bf16):
     plan = eng.dp.comm_plan()
     assert plan["n_buckets"] == len(eng.dp.buckets) and len(plan["bucket_bytes"]) == plan["n_buckets"]
     assert plan["wire_dtype"] == ("bf16" if bf16 else "fp32")
+    assert plan["comm_backend"] == ("rccl-native" if comm == "rccl" else "c10d")
+    if comm == "rccl":
+        if zero1:
+            eng.dp.wait_gathers()  # the parameter all-gathers are waited on by the NEXT forward
+        assert eng.dp.native.pending() == 0  # every collective's ticket was waited on
     if zero1:
         eng.opt.consolidate()
         st = eng.opt.state_dict()
@@ -250,10 +257,11 @@ def test_gpu_zero1_generate_after_step(tmp_path):
     assert torch.equal(r["out"], r["ref"])
 
 
+@pytest.mark.parametrize("comm", ["c10d", "rccl"])
 @pytest.mark.parametrize("zero1,bf16", [(False, False), (False, True), (True, False), (True, True)])
-def test_gpu_rccl_one_rank_collective_paths(tmp_path, zero1, bf16):
+def test_gpu_rccl_one_rank_collective_paths(tmp_path, zero1, bf16, comm):
     ctx = mp.get_context("spawn")
-    p = ctx.Process(target=_worker_rccl1, args=(_port(), str(tmp_path), zero1, bf16))
+    p = ctx.Process(target=_worker_rccl1, args=(_port(), str(tmp_path), zero1, bf16, comm))
     p.start()
     p.join(timeout=100)
     if p.is_alive():
@@ -282,7 +290,7 @@ def test_gpu_rccl_one_rank_collective_paths(tmp_path, zero1, bf16):
     assert cos > 0.995, cos
 
 
-def _worker_nccl2(rank, world, port, out_dir, zero1):
+def _worker_nccl2(rank, world, port, out_dir, zero1, comm="c10d"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import torch.distributed as dist
@@ -292,7 +300,7 @@ def _worker_nccl2(rank, world, port, out_dir, zero1):
 
     info = D.init_distributed(device="cuda", backend="nccl")
     assert info.backend == "nccl" and dist.get_world_size() == world
-    eng = StepEngine(_model(), lr=1e-3, grad_clip=1.0, bucket_mb=0.5, zero1=zero1)
+    eng = StepEngine(_model(), lr=1e-3, grad_clip=1.0, bucket_mb=0.5, zero1=zero1, comm=comm)
     x, y = _batch()
     per = x.shape[0] // world
     xs = x[rank * per:(rank + 1) * per].cuda()
@@ -313,13 +321,16 @@ def _worker_nccl2(rank, world, port, out_dir, zero1):
 
 
 @pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs 2 GPUs (RCCL over xGMI)")
+@pytest.mark.parametrize("comm", ["c10d", "rccl"])
 @pytest.mark.parametrize("zero1", [False, True])
-def test_gpu_nccl_two_gpus_match_single_process(tmp_path, zero1):
+def test_gpu_nccl_two_gpus_match_single_process(tmp_path, zero1, comm):
     """Two ranks on two GPUs over RCCL: the N-GPU step equals the 1-process step on the
-    concatenated batch, and the ranks stay bit-identical (DP all-reduce and ZeRO-1 paths)."""
+    concatenated batch, and the ranks stay bit-identical (DP all-reduce and ZeRO-1 paths; c10d's
+    communicator and the engine's own)."""
     ctx = mp.get_context("spawn")
     port = _port()
-    procs = [ctx.Process(target=_worker_nccl2, args=(r, 2, port, str(tmp_path), zero1)) for r in range(2)]
+    procs = [ctx.Process(target=_worker_nccl2, args=(r, 2, port, str(tmp_path), zero1, comm))
+             for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
