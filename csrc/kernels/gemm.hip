@@ -260,9 +260,53 @@ template <class CF>
 constexpr bool staged_dbias() { return 64 % (CF::WTN / 8) == 0; }
 
 // LDS -> global half of the staged epilogue for rows [mr, mr + 16 CHF) of the wave tile
+// Whole-tile bf16 copy-out (no side input, no bounds checks): a lane's pieces are RPI rows apart
+// at a fixed column, so its LDS and global addresses advance by constant strides (one base each,
+// immediates / one add per piece), and the LDS reads go out G at a time ahead of their stores.
+// Read-then-store per piece waited out each ds_read's latency before its store: 4.1-5.0k of the
+// W4 tile's ~8k epilogue cycles at K = 768 (tools/gemm_stamps.hip with -DMG_GEMM_EPI_STAMPS).
+template <int EPI, int S, int CHF, int PR, int IT, bool NT>
+MG_DEVICE void staged_copy_out(const GemmArgs& args, const char* st, int mr, int nw, int lane) {
+  constexpr int RPI = 64 / PR, G = 8;
+  static_assert(IT % G == 0, "pieces per lane must be a multiple of the read group");
+  const int r0 = lane / PR, p = lane % PR;
+  const char* lrow = st + r0 * S + p * 16;
+  const long off0 = (long)(mr + r0) * args.ldc + nw + p * 8;
+  bf16_t* gc = reinterpret_cast<bf16_t*>(args.C) + off0;
+  bf16_t* ga = EPI == 2 ? args.aux + off0 : nullptr;
+  const long rs = (long)RPI * args.ldc;
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int g0 = 0; g0 < IT; g0 += G) {
+    uint4 y[G], z[EPI == 2 ? G : 1];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      y[u] = *reinterpret_cast<const uint4*>(lrow + (g0 + u) * RPI * S);
+      if constexpr (EPI == 2) z[u] = *reinterpret_cast<const uint4*>(lrow + CHF * 16 * S + (g0 + u) * RPI * S);
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const long o = (long)(g0 + u) * rs;
+      if constexpr (NT) {
+        __builtin_nontemporal_store(v4u{y[u].x, y[u].y, y[u].z, y[u].w}, reinterpret_cast<v4u*>(gc + o));
+        if constexpr (EPI == 2)
+          __builtin_nontemporal_store(v4u{z[u].x, z[u].y, z[u].z, z[u].w}, reinterpret_cast<v4u*>(ga + o));
+      } else {
+        *reinterpret_cast<uint4*>(gc + o) = y[u];
+        if constexpr (EPI == 2) *reinterpret_cast<uint4*>(ga + o) = z[u];
+      }
+    }
+  }
+}
+
 template <class CF, int EPI, bool F32, int S, int CHF, int PR, int IT, bool CHECK>
 MG_DEVICE void staged_rows(const GemmArgs& args, const char* st, const uint4 (&sd)[F32 ? IT : 1], int mr,
                            int nw, int nlim, int lane, float (&cs)[8]) {
+  if constexpr (!F32 && !CHECK && 64 % PR == 0 && IT % 8 == 0) {
+    if (args.nt_out) staged_copy_out<EPI, S, CHF, PR, IT, true>(args, st, mr, nw, lane);
+    else staged_copy_out<EPI, S, CHF, PR, IT, false>(args, st, mr, nw, lane);
+    return;
+  }
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     const int e = it * 64 + lane, r = e / PR, p = e % PR;
@@ -331,7 +375,8 @@ MG_DEVICE void staged_rows(const GemmArgs& args, const char* st, const uint4 (&s
 
 template <class CF, int EPI, int LDSW>
 MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int m0, int n0,
-                               int wm, int wn, int wid, int lane, char* smem) {
+                               int wm, int wn, int wid, int lane, char* smem,
+                               unsigned long long* est = nullptr) {
   constexpr bool F32 = EPI == 3 || EPI == 4 || EPI == 5;  // staged before a bf16 side input is applied
   constexpr int PL = EPI == 2 ? 2 : 1;           // planes: y (+ GELU' for EPI 2)
   constexpr int S = CF::WTN * (F32 ? 4 : 2) + 16;  // row stride: rows 4 banks apart (b64/b128 writes)
@@ -401,10 +446,19 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
           *reinterpret_cast<uint2*>(row + col * 2) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
       }
     }
+#ifdef MG_GEMM_EPI_STAMPS
+    if (est && c == 0) est[0] = __builtin_amdgcn_s_memtime();  // fragments -> LDS issued
+#endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifdef MG_GEMM_EPI_STAMPS
+    if (est && c == 0) est[1] = __builtin_amdgcn_s_memtime();  // LDS writes landed
+#endif
     if (full) staged_rows<CF, EPI, F32, S, CHF, PR, IT, false>(args, st, sd, mw + c * CHF * 16, nw, nlim, lane, cs);
     else staged_rows<CF, EPI, F32, S, CHF, PR, IT, true>(args, st, sd, mw + c * CHF * 16, nw, nlim, lane, cs);
     asm volatile("" ::: "memory");  // the next pass's LDS writes stay behind these reads
+#ifdef MG_GEMM_EPI_STAMPS
+    if (est) est[2] = __builtin_amdgcn_s_memtime();  // staged reads + global stores issued
+#endif
   }
   if constexpr (EPI == 4 && staged_dbias<CF>()) {
     if (args.dbias) {  // kernel argument: uniform over the workgroup
@@ -435,10 +489,10 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
 // LDSW: LDS bytes each wave may use for the staged form (the K-loop's buffers are free by then).
 template <class CF, int EPI, bool OUTF32, int LDSW>
 MG_DEVICE void epilogue(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int m0, int n0, int wm,
-                        int wn, int wid, int lane, char* smem) {
+                        int wn, int wid, int lane, char* smem, unsigned long long* est = nullptr) {
   if constexpr (!OUTF32) {
     if (EPI != 4 || !args.dbias || staged_dbias<CF>()) {
-      epilogue_staged<CF, EPI, LDSW>(args, acc, m0, n0, wm, wn, wid, lane, smem);
+      epilogue_staged<CF, EPI, LDSW>(args, acc, m0, n0, wm, wn, wid, lane, smem, est);
       return;
     }
   }
@@ -1149,7 +1203,11 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
   W4_STAMP(8);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
+#ifdef MG_GEMM_EPI_STAMPS
+  epilogue<CF, EPI, OUTF32, WK::SMEM / 4>(args, acc, m0, n0, wm, wn, wid, lane, smem, st);
+#else
   epilogue<CF, EPI, OUTF32, WK::SMEM / 4>(args, acc, m0, n0, wm, wn, wid, lane, smem);
+#endif
 #ifdef MG_GEMM_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stores drained
   W4_STAMP(9);

@@ -3,6 +3,7 @@
 // the ping-pong kernel's K-tile MG_GEMM_STAMPS, the median cycles of each segment over all waves:
 //   reads+DMA issue | vmcnt wait | barrier 1 | lgkmcnt wait | MFMA | barrier 2 (next phase start)
 // Build: hipcc --offload-arch=gfx950 -O3 -DMG_GEMM_STAMPS=20 -Icsrc/include tools/gemm_stamps.hip
+// (-DMG_GEMM_STAMPS=1000 -DMG_GEMM_EPI_STAMPS: W4 epilogue segments instead of a K-tile's)
 #include "../csrc/kernels/gemm.hip"
 
 namespace mg {
@@ -70,6 +71,10 @@ int main(int argc, char** argv) {
     for (int k = 0; k < 5; ++k) printf(" %s=%lld", wseg[k], med(k, k + 1));
     printf("\nper tile: prologue=%lld main_loop=%lld epilogue=%lld (K-tiles %d)\n", med(6, 7), med(7, 8),
            med(8, 9), K / 64);
+#ifdef MG_GEMM_EPI_STAMPS
+    printf("epilogue: to-LDS issue=%lld LDS wait=%lld reads+stores issue=%lld store drain=%lld\n", med(8, 0),
+           med(0, 1), med(1, 2), med(2, 9));
+#endif
     // wall time per CU round: first start to last end over all blocks
     unsigned long long lo = ~0ull, hi = 0;
     for (int bl = 0; bl < blocks; ++bl) {
