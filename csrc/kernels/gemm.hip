@@ -299,12 +299,59 @@ MG_DEVICE void staged_copy_out(const GemmArgs& args, const char* st, int mr, int
   }
 }
 
+// Whole-tile fp32-staged output with a bf16 side input (EPI 3: + residual, EPI 4: x GELU'), same
+// addressing as staged_copy_out; the fp32 pieces are read G at a time ahead of their math and
+// stores.  The side input `sd` was loaded for the whole pass before the staging.
+template <class CF, int EPI, int S, int PR, int IT, bool NT>
+MG_DEVICE void staged_side_out(const GemmArgs& args, const char* st, const uint4 (&sd)[IT], int mr, int nw,
+                               int lane, float (&cs)[8]) {
+  constexpr int RPI = 64 / PR, G = 2;  // 4 spilled at EPI 4 (the pass's side input holds 64 VGPRs)
+  const int r0 = lane / PR, p = lane % PR;
+  const char* lrow = st + r0 * S + p * 32;
+  bf16_t* gc = reinterpret_cast<bf16_t*>(args.C) + (long)(mr + r0) * args.ldc + nw + p * 8;
+  const long rs = (long)RPI * args.ldc;
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int g0 = 0; g0 < IT; g0 += G) {
+    float4 a[G], b[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      a[u] = *reinterpret_cast<const float4*>(lrow + (g0 + u) * RPI * S);
+      b[u] = *reinterpret_cast<const float4*>(lrow + (g0 + u) * RPI * S + 16);
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      float v[8] = {a[u].x, a[u].y, a[u].z, a[u].w, b[u].x, b[u].y, b[u].z, b[u].w};
+      const uint4 sv = sd[g0 + u];
+      const uint32_t w[4] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float s = bf2f((w[k >> 1] >> (16 * (k & 1))) & 0xffffu);
+        v[k] = EPI == 3 ? v[k] + s : v[k] * s;
+      }
+      if constexpr (EPI == 4 && staged_dbias<CF>()) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) cs[k] += v[k];
+      }
+      const uint4 y = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
+      bf16_t* dst = gc + (long)(g0 + u) * rs;
+      if constexpr (NT) __builtin_nontemporal_store(v4u{y.x, y.y, y.z, y.w}, reinterpret_cast<v4u*>(dst));
+      else *reinterpret_cast<uint4*>(dst) = y;
+    }
+  }
+}
+
 template <class CF, int EPI, bool F32, int S, int CHF, int PR, int IT, bool CHECK>
 MG_DEVICE void staged_rows(const GemmArgs& args, const char* st, const uint4 (&sd)[F32 ? IT : 1], int mr,
                            int nw, int nlim, int lane, float (&cs)[8]) {
   if constexpr (!F32 && !CHECK && 64 % PR == 0 && IT % 8 == 0) {
     if (args.nt_out) staged_copy_out<EPI, S, CHF, PR, IT, true>(args, st, mr, nw, lane);
     else staged_copy_out<EPI, S, CHF, PR, IT, false>(args, st, mr, nw, lane);
+    return;
+  }
+  if constexpr ((EPI == 3 || EPI == 4) && !CHECK && 64 % PR == 0 && IT % 2 == 0) {
+    if (args.nt_out) staged_side_out<CF, EPI, S, PR, IT, true>(args, st, sd, mr, nw, lane, cs);
+    else staged_side_out<CF, EPI, S, PR, IT, false>(args, st, sd, mr, nw, lane, cs);
     return;
   }
 #pragma unroll
