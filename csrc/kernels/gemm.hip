@@ -1330,7 +1330,9 @@ int pick_config(int M, int N, int K, int layout) {
   // shape (bench/dgrad_nn_vs_nt.py, M = 65536: proj 84 / PP 97 us, fc 251 / 290, qkv 182 / 210,
   // fc2 + GELU' 344 / 362), and faster than NT against a transposed weight copy
   if (layout == 1) return t256 >= 256 ? 5 : 1;
-  if ((long)M * N < (1L << 20)) return 1;
+  // tiny outputs (gpt-mini) on T128; from 512 x 512 up the split-K cost model decides: the 768 x 768
+  // attention-projection gradient at 131k tokens runs 164 us on W4 vs 181 on T128 (bench_wgrad.py)
+  if ((long)M * N < (1L << 18)) return 1;
   // wgrad: W4 (256^2 tiles, one block per CU, split-K over 256 slots) unless T128 (128^2, two
   // blocks per CU, 512 slots) quantises so much better that it pays for its ~15 % lower per-CU
   // rate.  Both sides through the split-K cost model (rounds x (K-tiles per block + overhead)); a
