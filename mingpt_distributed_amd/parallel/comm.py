@@ -22,6 +22,7 @@ c10d stays the default: the native path is exercised on one GPU (a one-rank comm
 """
 from __future__ import annotations
 
+import atexit
 import os
 from typing import Optional
 
@@ -81,6 +82,9 @@ class RcclCommunicator:
         with torch.cuda.device(device):
             self.handle = int(self._C.comm_create(box[0], self.world, self.rank, device.index))
         self.stream = torch.cuda.ExternalStream(int(self._C.comm_stream_ptr(self.handle)), device=device)
+        # tear RCCL down before the interpreter (and torch's own atexit teardown of HIP / c10d):
+        # atexit runs handlers last-registered first, and this one is registered after torch's
+        atexit.register(self.close)
 
     @property
     def version_str(self) -> str:
@@ -112,6 +116,7 @@ class RcclCommunicator:
         return int(self._C.comm_pending(self.handle))
 
     def close(self):
+        """Destroy the RCCL communicator (idempotent; its comm stream stays, see rccl_comm.cpp)."""
         if getattr(self, "handle", None):
             self._C.comm_destroy(self.handle)
             self.handle = None
