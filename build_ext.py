@@ -33,6 +33,7 @@ COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-un
                 "-I" + os.path.join(ROOT, "csrc", "include"), "-ffp-contract=fast"]
 
 
+
 def _torch_paths():
     import torch
     from torch.utils.cpp_extension import include_paths

@@ -37,6 +37,12 @@ struct AttnArgs {
   float* dbias;        // bwd key-block mode: += column sums of dK / dV into [D, 3D) (qkv bias grad), or null
 };
 
+// 16-column MFMA k-steps a head dim is instantiated with: {1, 2, 3, 4, 6, 8}
+inline int nks_for(int hd) {
+  const int k = (hd + 15) / 16;
+  return k <= 4 ? k : (k <= 6 ? 6 : 8);
+}
+
 MG_DEVICE float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }  // v_exp_f32, no denorm fixup
 
 // 32-bit avalanche mixer (xorshift-multiply, "lowbias32" constants): a bijection with good
@@ -52,6 +58,18 @@ MG_DEVICE uint32_t mix32(uint32_t x) {
 inline uint32_t mix32_host(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
   return x;
+}
+
+// ------------------------------------------------------------------------------- forward
+// buffer descriptor over [base + off, base + total): reads past the end return 0.  The inputs are
+// readfirstlane'd so the compiler sees a uniform descriptor (no waterfall loop per load).
+MG_DEVICE __amdgpu_buffer_rsrc_t kv_rsrc(const bf16_t* base, uint64_t total, uint64_t off) {
+  const uint64_t p = reinterpret_cast<uint64_t>(base) + off;
+  const uint64_t left = off < total ? total - off : 0;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)(left < 0xffffffffull ? left : 0xffffffffull));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
 }
 
 MG_DEVICE bf16x8 lds_row_at(const char* base, int o) { return *reinterpret_cast<const bf16x8*>(base + o); }

@@ -1,5 +1,5 @@
-// Causal flash attention for training on gfx950 (CDNA4, MI355X): dropout keep-bit generator,
-// forward and backward.  (Decode: attention.hip.)
+// Causal flash attention backward for training on gfx950 (CDNA4, MI355X).  (Dropout keep bits and
+// the forward: attention_fwd.hip; decode: attention.hip.)
 //
 // Replaces the reference's nn.MultiheadAttention math path
 // (/root/reference/mingpt/model.py:147-165: in-proj split, q*scale, baddbmm with the [T,T] mask,
@@ -37,355 +37,6 @@ using namespace mg;
 using namespace mg::attn;
 
 namespace {
-
-#ifndef MG_FWD_PAIR
-#define MG_FWD_PAIR 1  // forward workgroup = two query blocks (heaviest + lightest), XCD-grouped
-#endif
-
-// ------------------------------------------------------------------------------- dropout bits
-// Keep bits (keep iff random byte >= thr) as "row words": word (bh, j, q), j = 2 * tile + h, covers
-// the 32 scores one forward lane holds for query q in 64-key tile `tile`, half h: value
-// e = 16 * sub + r  <->  key 64 * tile + 32 * sub + 4 * h + (r & 3) + 8 * (r >> 2), at bit
-// drop_bit(e) = 8 (e & 3) + (e >> 2).  Stored [bh][j][q]: lanes of consecutive queries read
-// consecutive words in both passes; the forward tests a compile-time bit, the backward a per-lane
-// one.  Randomness: one lowbias32 mix of the word index and seed, then xorshift32 steps -- shifts
-// and xors only (32-bit integer multiplies are quarter rate).
-//   Tried and removed: the same bits also transposed (32 ballots per wave) into per-register SGPR
-// lane masks so the forward drops a score with ONE v_cndmask_b32: at B = 128 the mask kernel went
-// 106 -> 277 us and the forward gained ~20 us (scalar loads, SGPR spills).
-__global__ __launch_bounds__(256) void attn_dropmask_kernel(uint32_t* __restrict__ dmask,
-                                                            int BH, int T, int ntw, int ng, int nt,
-                                                            uint64_t seed,
-                                                            const uint64_t* __restrict__ sofs,
-                                                            uint32_t thr) {
-  // grid (BH, ceil(ng / 4)); wave -> query group G (32 queries x 2 halves on its 64 lanes), tiles
-  // up to the group's diagonal (the forward and backward read no word past it); 32-bit index math
-  const int bh = blockIdx.x;
-  const int G = blockIdx.y * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (G >= ng) return;
-  const int lane = threadIdx.x & 63;
-  const int q = 32 * G + (lane & 31), h = lane >> 5;
-  const uint64_t sd = eff_seed(seed, sofs);
-  const uint32_t key = (uint32_t)sd ^ mix32((uint32_t)(sd >> 32) + 0x9E3779B9u);
-  const uint32_t kadd = (thr <= 128 ? 128u - thr : 256u - thr) * 0x01010101u;
-  const int tmax = min(nt - 1, G >> 1);
-  for (int t = 0; t <= tmax; ++t) {
-    const int j = 2 * t + h;
-    uint32_t bits = 0;
-    if (q < T) {
-      const uint32_t i = (uint32_t)((bh * ntw + j) * T + q);  // the word's index (wraps past 2^32: fine)
-      uint32_t x = mix32(i ^ key) | 1u;
-#pragma unroll
-      for (int w = 0; w < 8; ++w) {
-        x ^= x << 13;
-        x ^= x >> 17;
-        x ^= x << 5;
-        // SWAR: bit 7 of byte b <- (byte >= thr); value e = 4 w + b lands at bit 8 b + w
-        const uint32_t y = (x & 0x7f7f7f7fu) + kadd;
-        const uint32_t k7 = (thr <= 128 ? (y | x) : (y & x)) & 0x80808080u;
-        bits |= k7 >> (7 - w);
-      }
-      dmask[((long)bh * ntw + j) * T + q] = bits;
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------- forward
-// buffer descriptor over [base + off, base + total): reads past the end return 0.  The inputs are
-// readfirstlane'd so the compiler sees a uniform descriptor (no waterfall loop per load).
-MG_DEVICE __amdgpu_buffer_rsrc_t kv_rsrc(const bf16_t* base, uint64_t total, uint64_t off) {
-  const uint64_t p = reinterpret_cast<uint64_t>(base) + off;
-  const uint64_t left = off < total ? total - off : 0;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
-  const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)(left < 0xffffffffull ? left : 0xffffffffull));
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
-}
-
-// One 64-key tile for one wave's 32 queries: S'^T = K Q^T - m (the running max m rides in as the
-// MFMA's C operand), p = exp2(S'), O^T += V^T (Z P)^T.  There is no per-tile row max: m moves
-// only when a tile's partial row sum leaves [lo, 2^60] (lo = 2^-60 on a block's first tile, where
-// m starts at 0, else 0) -- then the tile is recomputed against its row max (regrow; rare: bf16 P
-// and the fp32 O / l accumulators hold p up to 2^60 exactly as well as p near 1).
-template <int NKS, bool MASK, bool DROP>
-MG_DEVICE void fwd_tile(const char* sk, const char* sv, const int (&ko)[NKS], const bf16x8 (&qf)[NKS],
-                        f32x16 (&o)[(NKS + 1) / 2], f32x16& negm, float& m, float& l, bool first,
-                        uint32_t kw, int lim, int ta0, int tb0, int ta1, int tb1) {
-  constexpr int NO = (NKS + 1) / 2;
-  constexpr int HALF = 64 * ROWB;
-  f32x16 s[2];
-  auto scores = [&](int lim) {
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_at(sk + sub * 32 * ROWB, ko[0]), qf[0], negm, 0, 0, 0);
-#pragma unroll
-      for (int ks = 1; ks < NKS; ++ks)
-        s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_at(sk + sub * 32 * ROWB, ko[ks]), qf[ks],
-                                                         s[sub], 0, 0, 0);
-    }
-    if constexpr (MASK) {  // key = k0 + c(sub, r) + 4 h32, c a constant: one compare per score
-      // lim made opaque here: the compares cannot be hoisted above the MFMAs (32 compare
-      // results held in SGPR pairs meanwhile were most of this kernel's scalar pressure)
-      asm volatile("" : "+v"(lim));
-#pragma unroll
-      for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          s[sub][r] = (sub * 32 + (r & 3) + 8 * (r >> 2) > lim) ? kNegBig : s[sub][r];
-    }
-  };
-  auto expsum = [&]() {
-    float rs = 0.f;
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = fexp2(s[sub][r]);
-        rs += p;
-        s[sub][r] = p;
-      }
-    return rs;
-  };
-  scores(lim);
-  float rs = expsum();
-  const float lo = first ? 8.673617379884035e-19f : 0.f;  // 2^-60
-  if (__builtin_expect(__any(!(rs <= 1.152921504606847e18f && rs >= lo)), 0)) {  // 2^60; inf / nan
-    // recompute S' (K is still in LDS) instead of keeping it live; an opaque copy of lim keeps
-    // the compiler from holding the first pass's 32 mask compares (64 SGPRs) for this one
-    int lim2 = lim;
-    asm volatile("" : "+v"(lim2));
-    scores(lim2);
-    float mx = s[0][0];
-#pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s[0][r]);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[1][r]);
-    mx = max_xor32(mx);
-    // a block's first tile may move m down as well (nothing accumulated yet); later tiles up only
-    const float d = first ? mx : fmaxf(mx, 0.f);
-    const float alpha = first ? 1.f : fexp2(-d);
-    l *= alpha;
-#pragma unroll
-    for (int n = 0; n < NO; ++n) o[n] *= alpha;
-    m += d;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) negm[r] = -m;
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s[sub][r] -= d;
-    rs = expsum();
-  }
-  l += rs;
-  // dropout for O only (l sums the undropped P); the keep scale is applied to O at the end
-#pragma unroll
-  for (int sub = 0; sub < 2; ++sub) {
-    if constexpr (DROP) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int bit = 8 * (r & 3) + (r >> 2) + 4 * sub;  // drop_bit(16 sub + r)
-        const int keep = (int)(kw << (31 - bit)) >> 31;  // sign-extended bit: one v_bfe_i32
-        s[sub][r] = __int_as_float(__float_as_int(s[sub][r]) & keep);
-      }
-    }
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      const bf16x8 pf = pack_frag(s[sub], st);
-      const int rb = (sub * 32 + 16 * st) * ROWB;  // 16-row aligned: an immediate
-#pragma unroll
-      for (int n = 0; n < NO; ++n) {
-        const char* vb = sv + (n >> 1) * HALF + rb;
-        o[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            (n & 1) ? lds_tr_at(vb, ta1, tb1) : lds_tr_at(vb, ta0, tb0), pf, o[n], 0, 0, 0);
-      }
-    }
-  }
-}
-
-// Forward, FA2 structure mapped onto MI355X:
-//  * workgroup = 4 waves; a query block = 128 queries of one (b, h), each wave 32 of them; the
-//    workgroup runs TWO query blocks of its (b, h) back to back, the i-th heaviest and the i-th
-//    lightest (causal work (nqb - 1 - i) + i + 2 tiles pairs: every workgroup the same), and the
-//    K/V tile stream continues across the seam (the second block's first tile is prefetched
-//    during the first block's last).
-//  * XCD-aware grid: the workgroups of one (b, h) are dispatched 8 apart, i.e. onto one XCD
-//    under round-robin placement, within one dispatch window: they share K/V through that XCD's
-//    L2 instead of each pulling them from HBM (speed only; correctness never depends on it).
-//  * Q fragments live in VGPRs, pre-multiplied by log2(e)/sqrt(hd): S comes out of the MFMA in
-//    the log2 domain; the running max enters as the MFMA's C operand, so p = exp2(S') is ONE
-//    v_exp_f32 per score and no per-tile row max exists (fwd_tile).
-//  * K/V tiles of 64 keys staged through LDS (double buffer, register staging: tile t+1's global
-//    loads are in flight during tile t's MFMAs), one barrier per tile.
-//  * S^T = K Q^T with v_mfma_f32_32x32x16_bf16 (query on the lane: the row sums are lane-local;
-//    the two 32-key halves meet once, after the last tile); P converted to bf16 in registers is
-//    the B operand of O^T = V^T P^T, V^T read with ds_read_b64_tr_b16 in the matching key order.
-//  * dropout: lane masks from attn_dropmask_kernel (scalar loads, one v_cndmask per score).
-template <int NKS, bool DROP>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
-  constexpr int NH = (NKS + 3) / 4;   // 64-column halves of the LDS images
-  constexpr int NO = (NKS + 1) / 2;   // 32-column O^T accumulator tiles
-  constexpr int HALF = 64 * ROWB;     // one 64-row, 64-column image
-  constexpr int TILE = NH * HALF;     // one K or V tile
-  constexpr int NC = 2 * NH;          // 16-byte chunks per thread per tile per matrix
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // K0 V0 K1 V1
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int h32 = lane >> 5, l32 = lane & 31;
-  const int nqb = (a.T + 127) / 128;
-  const int npair = (nqb + 1) / 2;
-  const int BH = a.B * a.H;
-  int bh, pr;
-  if (!MG_FWD_PAIR) {  // one query block per workgroup, heaviest blocks first
-    bh = blockIdx.x % BH;
-    pr = blockIdx.x / BH;
-  } else if ((BH & 7) == 0) {  // (b, h)'s workgroups 8 apart: one XCD
-    const int x = blockIdx.x & 7, rest = blockIdx.x >> 3;
-    pr = rest % npair;
-    bh = (rest / npair) * 8 + x;
-  } else {
-    pr = blockIdx.x % npair;
-    bh = blockIdx.x / npair;
-  }
-  const int b = bh / a.H, hh = bh % a.H;
-  const long ld = 3L * a.D;
-  const bf16_t* Qg = a.qkv + (long)b * a.T * ld + hh * a.hd;
-  const bf16_t* Kg = Qg + a.D;
-  const bf16_t* Vg = Qg + 2 * a.D;
-  // the pair's query blocks, heavier first; the middle block of an odd count runs alone
-  const int qbA = nqb - 1 - pr, qbB = pr;
-  const bool two = MG_FWD_PAIR && qbB < qbA;
-  const int ntA = (min(a.T, qbA * 128 + 128) + 63) / 64;
-  const int ntB = two ? (min(a.T, qbB * 128 + 128) + 63) / 64 : 0;
-  const int ng = (a.T + 31) / 32, nt = (a.T + 63) / 64;
-
-  // tile staging: chunk c of this thread -> (half, row, 16-byte column chunk), offsets once.  The
-  // loads are buffer loads through a per-tile descriptor (base = the tile's first key row, extent
-  // = the rest of qkv): no per-lane bounds branches or 64-bit address math per tile.  Rows past T
-  // read the next sequence's (finite) rows or, past the tensor, zeros; their scores are masked
-  // (the tile takes the masked body) and their p is 0.  Columns past hd read the neighbouring
-  // head: K there meets zero Q columns, V there only feeds O columns that are never stored.
-  uint32_t voff[NC], sdst[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const int idx = threadIdx.x + 256 * c;
-    const int hf = idx >> 9, rem = idx & 511;
-    voff[c] = (uint32_t)(((rem >> 3) * ld + hf * 64 + (rem & 7) * 8) * 2);
-    sdst[c] = hf * HALF + lds_off(rem >> 3, rem & 7);
-  }
-  const uint64_t kv_bytes = (uint64_t)a.B * a.T * ld * 2;  // the whole qkv tensor
-  const uint64_t kbase = (uint64_t)((const char*)Kg - (const char*)a.qkv);
-  auto load_tile = [&](uint4 (&rk)[NC], uint4 (&rv)[NC], int k0) {
-    const uint64_t off = kbase + (uint64_t)k0 * ld * 2;
-    const __amdgpu_buffer_rsrc_t dk = kv_rsrc(a.qkv, kv_bytes, off);
-    const __amdgpu_buffer_rsrc_t dv = kv_rsrc(a.qkv, kv_bytes, off + (uint64_t)a.D * 2);
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      rk[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(dk, voff[c], 0, 0));
-      rv[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(dv, voff[c], 0, 0));
-    }
-  };
-  auto store_tile = [&](char* dst, const uint4 (&rk)[NC], const uint4 (&rv)[NC]) {
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      *reinterpret_cast<uint4*>(dst + sdst[c]) = rk[c];
-      *reinterpret_cast<uint4*>(dst + TILE + sdst[c]) = rv[c];
-    }
-  };
-
-  // per-lane fragment offsets: K rows l32 (+32 per sub: an immediate), chunk 2 ks + h32;
-  // V^T transposed reads rows 4 h32 + q (+8), columns (n & 1) * 32 + cb + 4 p
-  int ko[NKS];
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) ko[ks] = (ks >> 2) * HALF + lds_off(l32, (2 * ks + h32) & 7);
-  const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-  const int ta0 = tr_off(4 * h32 + trq, trc), tb0 = tr_off(8 + 4 * h32 + trq, trc);
-  const int ta1 = tr_off(4 * h32 + trq, 32 + trc), tb1 = tr_off(8 + 4 * h32 + trq, 32 + trc);
-
-  bf16x8 qf[NKS];
-  f32x16 o[NO], negm;
-  float m = 0.f, l = 0.f;
-  int q0 = 0, myq = 0;
-  auto begin_block = [&](int qb) {  // Q fragments (k-step ks: columns 16 ks + 8 h32 .. +7), scaled
-    q0 = qb * 128;
-    myq = q0 + 32 * w + l32;
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      const int d = ks * 16 + 8 * h32;
-      uint4 u = (myq < a.T && d < a.hd) ? ld16(Qg + (long)myq * ld + d) : make_uint4(0, 0, 0, 0);
-      float f[8];
-      unpack8(u, f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] *= a.scale_log2;
-      qf[ks] = __builtin_bit_cast(bf16x8, pack8(f));
-    }
-#pragma unroll
-    for (int n = 0; n < NO; ++n) o[n] = f32x16{0};
-    negm = f32x16{0};
-    m = 0.f;
-    l = 0.f;
-  };
-  auto end_block = [&]() {
-    const float lt = sum_xor32(l);
-    if (myq < a.T) {
-      const float inv = (DROP ? a.dscale : 1.f) / lt;
-      if (h32 == 0) a.lse[(long)bh * a.T + myq] = m + log2f(lt);  // log2 domain
-      bf16_t* orow = a.out + ((long)b * a.T + myq) * a.D + hh * a.hd;
-#pragma unroll
-      for (int n = 0; n < NO; ++n)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int d = n * 32 + 8 * g + 4 * h32;
-          if (d < a.hd)
-            *reinterpret_cast<uint2*>(orow + d) = make_uint2(pack2(o[n][4 * g] * inv, o[n][4 * g + 1] * inv),
-                                                             pack2(o[n][4 * g + 2] * inv, o[n][4 * g + 3] * inv));
-        }
-    }
-  };
-
-  // row-word dropout: word (bh, 2 t + h32, q) of this lane's query, loaded one tile ahead
-  auto row_word = [&](int t, int q) -> uint32_t {
-    return a.dmask[((long)bh * (2 * nt) + 2 * t + h32) * a.T + min(q, a.T - 1)];
-  };
-  begin_block(qbA);
-  uint32_t kw_next = DROP ? row_word(0, myq) : 0u;
-  {
-    uint4 rk[NC], rv[NC];
-    load_tile(rk, rv, 0);
-    store_tile(smem, rk, rv);
-  }
-  __syncthreads();
-  const int nall = ntA + ntB;
-  for (int it = 0; it < nall; ++it) {
-    const bool second = it >= ntA;
-    const int t = second ? it - ntA : it;
-    const char* sk = smem + (it & 1) * 2 * TILE;
-    const char* sv = sk + TILE;
-    const bool more = it + 1 < nall;
-    uint4 rk[NC], rv[NC];
-    if (more) load_tile(rk, rv, (it + 1 == ntA ? 0 : t + 1) * 64);
-    uint32_t kw_cur = kw_next;
-    if (DROP && more) {  // next tile's keep words, a tile ahead (latency hidden)
-      const bool seam = it + 1 == ntA;
-      kw_next = row_word(seam ? 0 : t + 1, seam ? qbB * 128 + 32 * w + l32 : myq);
-    }
-    const int k0 = t * 64;
-    const int wave_q = q0 + 32 * w;
-    if (k0 <= wave_q + 31 && wave_q < a.T) {  // (a wave past the sequence end has nothing to do)
-      const int lim = min(myq, a.T - 1) - k0 - 4 * h32;
-      // causal / sequence-end mask only on the tiles that need it (separate bodies: a uniform
-      // branch inside one body got if-converted into compares + selects on every tile)
-      const bool diag = k0 + 63 > wave_q || k0 + 64 > a.T;
-      if (diag) fwd_tile<NKS, true, DROP>(sk, sv, ko, qf, o, negm, m, l, t == 0, kw_cur, lim, ta0, tb0, ta1, tb1);
-      else fwd_tile<NKS, false, DROP>(sk, sv, ko, qf, o, negm, m, l, t == 0, kw_cur, lim, ta0, tb0, ta1, tb1);
-    }
-    if (it + 1 == ntA) {  // seam: first block done, the second starts with the prefetched tile 0
-      end_block();
-      if (two) begin_block(qbB);
-    }
-    if (more) store_tile(smem + ((it + 1) & 1) * 2 * TILE, rk, rv);
-    __syncthreads();
-  }
-  if (two) end_block();
-}
 
 // =============================================================================== backward
 // delta[(b*H + h)*T + t] = sum_d dO * O.  One lane per 16-byte chunk (8 elements) of a head row,
@@ -1260,7 +911,6 @@ constexpr int bwd_smem() {
          (PERSIST ? (KSPLIT > 1 ? TILES : KW) * NTW * 16 * 64 * 4 : 0);
 }
 
-int nks_for(int hd);
 int nks_for_bwd(int hd) { return nks_for(hd); }
 
 int num_cus() {
@@ -1336,60 +986,9 @@ void launch_bwd(const AttnArgs& a, hipStream_t stream) {
     attn_bwd_kernel<NKS, KW, true><<<a.B * a.H, 64 * KW, smem_p, stream>>>(a);
 }
 
-int nks_for(int hd) {
-  const int k = (hd + 15) / 16;
-  return k <= 4 ? k : (k <= 6 ? 6 : 8);
-}
-
 }  // namespace
 
 namespace mg {
-
-// row words [B*H][2 ceil(T/64)][T] u32 (attn_dropmask_kernel)
-size_t attention_dropout_mask_words(int B, int T, int H) { return (size_t)B * H * T * 2 * ((T + 63) / 64); }
-
-int attention_dropout_threshold(float p) {
-  // 8-bit dropout threshold (as FlashAttention does): effective p = thr / 256
-  if (!(p > 0.f)) return 0;
-  int thr = (int)lrintf(p * 256.f);
-  return thr < 1 ? 1 : (thr > 255 ? 255 : thr);
-}
-
-void attention_dropout_mask(uint32_t* dmask, int B, int T, int H, float p, uint64_t seed,
-                            hipStream_t stream) {
-  const int thr = attention_dropout_threshold(p);
-  if (!thr) return;
-  const int ntw = 2 * ((T + 63) / 64), ng = (T + 31) / 32, nt = (T + 63) / 64;
-  attn_dropmask_kernel<<<dim3((unsigned)(B * H), (unsigned)cdiv(ng, 4)), 256, 0, stream>>>(
-      dmask, B * H, T, ntw, ng, nt, seed, graph_seed_ofs(), (uint32_t)thr);
-}
-
-template <int NKS>
-static void launch_fwd(const AttnArgs& a, int grid, hipStream_t stream) {
-  if (a.thr) attn_fwd_kernel<NKS, true><<<grid, 256, 0, stream>>>(a);
-  else attn_fwd_kernel<NKS, false><<<grid, 256, 0, stream>>>(a);
-}
-
-void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, uint32_t* dmask, int B, int T, int H,
-                   int hd, float p, uint64_t seed, hipStream_t stream) {
-  AttnArgs a{};
-  a.B = B; a.T = T; a.H = H; a.hd = hd; a.D = H * hd;
-  a.scale_log2 = 1.4426950408889634f / sqrtf((float)hd);
-  a.thr = dmask ? (uint32_t)attention_dropout_threshold(p) : 0u;
-  a.dscale = a.thr ? 256.f / (256.f - (float)a.thr) : 1.f;
-  a.qkv = qkv; a.out = out; a.lse = lse; a.dmask = dmask;
-  if (a.thr) attention_dropout_mask(dmask, B, T, H, p, seed, stream);
-  const int nqb = cdiv(T, 128);
-  const int grid = (MG_FWD_PAIR ? (nqb + 1) / 2 : nqb) * B * H;  // (pairs of) query blocks
-  switch (nks_for(hd)) {
-    case 1: launch_fwd<1>(a, grid, stream); break;
-    case 2: launch_fwd<2>(a, grid, stream); break;
-    case 3: launch_fwd<3>(a, grid, stream); break;
-    case 4: launch_fwd<4>(a, grid, stream); break;
-    case 6: launch_fwd<6>(a, grid, stream); break;
-    default: launch_fwd<8>(a, grid, stream); break;
-  }
-}
 
 void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse,
                    const uint32_t* dmask, float* delta, float* dq, bf16_t* dqkv, int B, int T, int H,

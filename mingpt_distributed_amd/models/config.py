@@ -110,7 +110,7 @@ class GPTConfig:
     def gpu_unsupported(self) -> Optional[str]:
         """Why the GPU kernels cannot run this config, or None.  Every kernel reads rows in
         16-byte (8 x bf16) vectors; the attention kernels take any head dim that is a multiple of 8
-        up to 128 (csrc/kernels/attention_train.hip ``nks_for``; decode: attention.hip)."""
+        up to 128 (csrc/include/attn_common.h ``nks_for``; decode: attention.hip)."""
         if self.n_embed is None or self.n_head is None:
             return "config not resolved"
         hd = self.n_embed // self.n_head

@@ -144,7 +144,7 @@ def test_attention_dropout_gradient_directional():
 
 def _dense_keep(mask, B, T, H):
     """Dense [B, H, T(query), T(key)] keep matrix from the keep-bit row words (layout and bit
-    order: attention_train.hip attn_dropmask_kernel; words of tiles past the diagonal are
+    order: attention_fwd.hip attn_dropmask_kernel; words of tiles past the diagonal are
     unspecified)."""
     ntw = 2 * ((T + 63) // 64)
     words = mask.view(B * H, ntw, T).to(torch.int64) & 0xFFFFFFFF  # [bh, j, q]
