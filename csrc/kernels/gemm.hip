@@ -40,7 +40,10 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int BK = 64;
-constexpr int GROUP_M = 8;
+#ifndef MG_GROUP_M
+#define MG_GROUP_M 8
+#endif
+constexpr int GROUP_M = MG_GROUP_M;  // row tiles per L2 group (blocks of a group share B column tiles)
 constexpr uint32_t kOOB = 0xFFFFFFF0u;
 
 template <int BM_, int BN_, int NWM_, int NWN_, int STAGES_ = 2>
