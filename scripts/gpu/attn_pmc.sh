@@ -11,7 +11,7 @@ i=0
 for P in "$P1" "$P2" "$P3"; do
   i=$((i + 1))
   ATTN_ITERS=2 timeout -s KILL 90 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$OUT/p$i" -o a \
-    -- python3 bench/dev/attn_prof.py > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; continue; }
+    -- python3 bench/dev/attn_prof.py > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
   for f in $(find "$OUT/p$i" -name '*counter_collection.csv'); do
     python scripts/pmc_summary.py "$f" attn_ > "$OUT/p$i.txt"; cat "$OUT/p$i.txt"
   done
