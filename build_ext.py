@@ -103,9 +103,26 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True, debug: bool 
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out, *objs,
               "-L" + tlib, "-Wl,-rpath," + tlib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
               "-ltorch_hip", "-ltorch_python", "-lamdhip64"])
+        bad = anon_undefined(out)
+        if bad:
+            os.remove(out)
+            raise RuntimeError(f"link produced unresolvable internal symbols (e.g. a kernel whose host "
+                               f"launch stub was not emitted): {bad[:5]}")
         if verbose:
             print(f"[build_ext] linked {os.path.relpath(out, ROOT)}", flush=True)
     return out
+
+
+def anon_undefined(so: str):
+    """Undefined symbols of ``so`` in an anonymous namespace (``_GLOBAL__N_``): nothing outside the
+    library can define them, so each one is a build bug that would only surface as an ImportError
+    on the GPU box (seen: a target builtin in a ``__global__`` template body made hipcc drop the
+    host launch stub of that instantiation).  Empty when ``nm`` is not available."""
+    try:
+        r = subprocess.run(["nm", "-D", "--undefined-only", so], capture_output=True, text=True)
+    except OSError:
+        return []
+    return [ln.split()[-1] for ln in r.stdout.splitlines() if "_GLOBAL__N_" in ln]
 
 
 def _torch_runtime_dir() -> str:
