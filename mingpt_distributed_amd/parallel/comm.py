@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import atexit
 import os
+import weakref
 from typing import Optional
 
 import torch
@@ -40,6 +41,12 @@ def comm_backend_default() -> str:
     if v not in ("c10d", "rccl"):
         raise ValueError(f"MINGPT_COMM must be c10d or rccl, not {v!r}")
     return v
+
+
+def _close_if_alive(ref):
+    c = ref()
+    if c is not None:
+        c.close()
 
 
 class Work:
@@ -83,8 +90,10 @@ class RcclCommunicator:
             self.handle = int(self._C.comm_create(box[0], self.world, self.rank, device.index))
         self.stream = torch.cuda.ExternalStream(int(self._C.comm_stream_ptr(self.handle)), device=device)
         # tear RCCL down before the interpreter (and torch's own atexit teardown of HIP / c10d):
-        # atexit runs handlers last-registered first, and this one is registered after torch's
-        atexit.register(self.close)
+        # atexit runs handlers last-registered first, and this one is registered after torch's.
+        # Through a weak reference, so the handler does not keep a dropped communicator (and its
+        # RCCL resources) alive until exit; __del__ closes it when it is collected
+        atexit.register(_close_if_alive, weakref.ref(self))
 
     @property
     def version_str(self) -> str:

@@ -250,3 +250,28 @@ def test_comm_backend_selection_cpu(tmp_path, monkeypatch):
     assert p.exitcode == 0
     msgs = (tmp_path / "msgs.txt").read_text().splitlines()
     assert "GPU" in msgs[0] and msgs[1] == "c10d"
+
+
+def test_comm_exit_handler_does_not_pin_communicator():
+    """The communicator's atexit teardown holds it only weakly: a dropped communicator is closed
+    by its own __del__ (freeing its RCCL resources then), and the exit handler skips it."""
+    import gc
+    import weakref
+
+    from mingpt_distributed_amd.parallel.comm import _close_if_alive
+
+    closed = []
+
+    class Fake:
+        def close(self):
+            closed.append(1)
+
+    f = Fake()
+    ref = weakref.ref(f)
+    _close_if_alive(ref)
+    assert closed == [1]
+    del f
+    gc.collect()
+    assert ref() is None
+    _close_if_alive(ref)
+    assert closed == [1]
