@@ -68,6 +68,13 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True, debug: bool 
     flags += os.environ.get("MG_EXTRA_FLAGS", "").split()  # kernel variant switches (A/B builds)
     bdir = BUILD + "_debug" if debug else BUILD
     os.makedirs(bdir, exist_ok=True)
+    # the objects' compile flags (MG_EXTRA_FLAGS variant switches included): a change rebuilds
+    # every object, so a variant build never leaves objects a later plain build would link
+    stamp = os.path.join(bdir, "flags.stamp")
+    key = " ".join(flags)
+    old = open(stamp).read() if os.path.exists(stamp) else None
+    if old != key:
+        force = True
     headers = glob.glob(os.path.join(ROOT, "csrc", "include", "*.h"))
     kernels = sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip")))
     kernels += sorted(glob.glob(os.path.join(ROOT, "csrc", "comm", "*.cpp")))  # host code (HIP runtime + RCCL)
@@ -97,6 +104,9 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True, debug: bool 
                 f.result()
                 if verbose:
                     print(f"[build_ext] compiled {os.path.relpath(futs[f], ROOT)}", flush=True)
+    if old != key:
+        with open(stamp, "w") as f:
+            f.write(key)
     out = DEBUG_SO if debug else os.path.join(PKG, "_C.so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     if force or _newer(out, objs):

@@ -640,6 +640,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("comm_broadcast", &comm_broadcast);
   m.def("comm_wait", &comm_wait);
   m.def("comm_pending", &mg::comm::pending);
+  m.def("comm_retire", &mg::comm::retire);
+  m.def("comm_query", &mg::comm::query);
   m.doc() = "mingpt_distributed_amd gfx950 kernels";
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);

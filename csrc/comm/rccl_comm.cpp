@@ -90,12 +90,16 @@ struct Comm {
   }
 };
 
-std::vector<std::unique_ptr<Comm>> g_comms;  // handle = index + 1; slots are never reused
+// handle = index + 1; slots are never reused.  Callers hold a shared_ptr copy for the whole call
+// (taken under g_mu), so destroy() -- reachable from a Python finaliser on any thread -- can drop
+// the slot while a call is inside enqueue()/wait() without freeing the Comm under it: the last
+// reference releases it after that call returns.
+std::vector<std::shared_ptr<Comm>> g_comms;
 
-Comm& get(int64_t h) {
+std::shared_ptr<Comm> get(int64_t h) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (h <= 0 || h > (int64_t)g_comms.size() || !g_comms[h - 1]) throw std::runtime_error("mg::comm: bad handle");
-  return *g_comms[h - 1];
+  return g_comms[h - 1];
 }
 
 struct DeviceScope {  // the communicator's device for the duration of a call
@@ -113,7 +117,8 @@ struct DeviceScope {  // the communicator's device for the duration of a call
 // comm stream after the compute stream's work so far -> collective -> completion ticket
 template <class F>
 int64_t enqueue(int64_t h, hipStream_t cs, F&& collective, const char* what) {
-  Comm& c = get(h);
+  const std::shared_ptr<Comm> cp = get(h);
+  Comm& c = *cp;
   std::lock_guard<std::mutex> lk(c.mu);
   DeviceScope ds(c.device);
   hipEvent_t before = c.event();
@@ -166,7 +171,7 @@ int64_t create(const std::string& uid, int nranks, int rank, int device) {
   if (!g_lib) throw std::runtime_error("mg::comm: load_rccl first");
   if ((int)uid.size() != kUniqueIdBytes) throw std::runtime_error("mg::comm: unique id must be 128 bytes");
   if (nranks < 1 || rank < 0 || rank >= nranks) throw std::runtime_error("mg::comm: bad rank / world size");
-  auto c = std::make_unique<Comm>();
+  auto c = std::make_shared<Comm>();
   c->device = device;
   c->nranks = nranks;
   c->rank = rank;
@@ -183,27 +188,31 @@ int64_t create(const std::string& uid, int nranks, int rank, int device) {
 }
 
 void destroy(int64_t h) {
-  std::unique_ptr<Comm> c;
+  std::shared_ptr<Comm> c;
   {
     std::lock_guard<std::mutex> lk(g_mu);
     if (h <= 0 || h > (int64_t)g_comms.size() || !g_comms[h - 1]) return;
     c = std::move(g_comms[h - 1]);
   }
+  std::lock_guard<std::mutex> lk(c->mu);  // a concurrent enqueue()/wait() on another thread finishes first
   DeviceScope ds(c->device);
   (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)g_fn.commDestroy(c->comm);
   for (auto& kv : c->tickets) (void)hipEventDestroy(kv.second);
   for (auto e : c->free_ev) (void)hipEventDestroy(e);
+  c->tickets.clear();
+  c->free_ev.clear();
+  c->comm = nullptr;
   // the comm stream is NOT destroyed: tensors the caller recorded on it (record_stream, so the
   // caching allocator does not hand their blocks out while a collective may still touch them)
   // make the allocator record events on this stream whenever they are freed -- possibly after
   // the communicator is gone.  One idle stream per communicator for the life of the process.
 }
 
-hipStream_t comm_stream(int64_t h) { return get(h).stream; }
-int nranks(int64_t h) { return get(h).nranks; }
-int device(int64_t h) { return get(h).device; }
-int rank(int64_t h) { return get(h).rank; }
+hipStream_t comm_stream(int64_t h) { return get(h)->stream; }
+int nranks(int64_t h) { return get(h)->nranks; }
+int device(int64_t h) { return get(h)->device; }
+int rank(int64_t h) { return get(h)->rank; }
 
 int64_t all_reduce(int64_t h, void* buf, size_t count, DType dt, hipStream_t cs) {
   return enqueue(h, cs, [&](Comm& c) {
@@ -230,7 +239,8 @@ int64_t broadcast(int64_t h, void* buf, size_t count, DType dt, int root, hipStr
 }
 
 void wait(int64_t h, int64_t ticket, hipStream_t s) {
-  Comm& c = get(h);
+  const std::shared_ptr<Comm> cp = get(h);
+  Comm& c = *cp;
   std::lock_guard<std::mutex> lk(c.mu);
   auto it = c.tickets.find(ticket);
   if (it == c.tickets.end()) throw std::runtime_error("mg::comm: unknown or already waited ticket");
@@ -240,10 +250,39 @@ void wait(int64_t h, int64_t ticket, hipStream_t s) {
   c.tickets.erase(it);
 }
 
+void retire(int64_t h, int64_t ticket) {
+  std::shared_ptr<Comm> cp;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (h <= 0 || h > (int64_t)g_comms.size() || !g_comms[h - 1]) return;  // destroyed: nothing to release
+    cp = g_comms[h - 1];
+  }
+  std::lock_guard<std::mutex> lk(cp->mu);
+  auto it = cp->tickets.find(ticket);
+  if (it == cp->tickets.end()) return;
+  // nobody will wait on it: the event goes back to the free list (a later re-record of a pending
+  // event is fine -- only a stream wait captures a record, and none will for this ticket)
+  cp->free_ev.push_back(it->second);
+  cp->tickets.erase(it);
+}
+
+int query(int64_t h, int64_t ticket) {
+  const std::shared_ptr<Comm> cp = get(h);
+  std::lock_guard<std::mutex> lk(cp->mu);
+  auto it = cp->tickets.find(ticket);
+  if (it == cp->tickets.end()) return -1;
+  DeviceScope ds(cp->device);
+  const hipError_t e = hipEventQuery(it->second);
+  if (e == hipSuccess) return 1;
+  if (e == hipErrorNotReady) return 0;
+  hip_check(e, "hipEventQuery");
+  return 0;
+}
+
 int pending(int64_t h) {
-  Comm& c = get(h);
-  std::lock_guard<std::mutex> lk(c.mu);
-  return (int)c.tickets.size();
+  const std::shared_ptr<Comm> cp = get(h);
+  std::lock_guard<std::mutex> lk(cp->mu);
+  return (int)cp->tickets.size();
 }
 
 }  // namespace comm

@@ -44,6 +44,12 @@ int64_t reduce_scatter(int64_t h, const void* in, void* out, size_t count_per_ra
 int64_t all_gather(int64_t h, const void* in, void* out, size_t count_per_rank, DType dt, hipStream_t cs);
 int64_t broadcast(int64_t h, void* buf, size_t count, DType dt, int root, hipStream_t cs);
 void wait(int64_t h, int64_t ticket, hipStream_t s);
+// release a ticket nobody will wait on (a dropped Work): its event returns to the free list, no
+// stream waits; a no-op for unknown tickets or a destroyed communicator
+void retire(int64_t h, int64_t ticket);
+// 1 if the ticket's collective has completed on the device, 0 if not yet, -1 if the ticket is
+// not outstanding (already waited / retired) -- diagnostics (bench.py's hang report)
+int query(int64_t h, int64_t ticket);
 // outstanding tickets (issued, not yet waited)
 int pending(int64_t h);
 

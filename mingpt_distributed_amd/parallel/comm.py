@@ -18,7 +18,11 @@ RCCL themselves instead:
   bucket, all-gather out of it, broadcast.
 
 c10d stays the default: the native path is exercised on one GPU (a one-rank communicator,
-``tests/test_comm_gpu.py``) but not yet measured across GPUs.
+``tests/test_comm_gpu.py``) and is **not yet verified at world > 1** (the pool's GPU boxes have
+one GPU; ``tests/test_dp_gpu.py::test_gpu_nccl_two_gpus_match_single_process[rccl]`` covers it
+on a multi-GPU node).  When an engine owns a native communicator, every collective of its step
+goes through it (the ZeRO-1 grad-norm all-reduce included), so one step never mixes two
+communicators' streams.
 """
 from __future__ import annotations
 
@@ -50,7 +54,10 @@ def _close_if_alive(ref):
 
 
 class Work:
-    """One collective in flight: ``wait()`` orders the caller's current stream after it."""
+    """One collective in flight: ``wait()`` orders the caller's current stream after it.  A Work
+    dropped without ``wait()`` (an exception between launch and finish, an engine closed with
+    buckets in flight) retires its ticket when collected, so the communicator's outstanding
+    tickets do not grow for its lifetime."""
 
     __slots__ = ("_comm", "_ticket")
 
@@ -63,7 +70,22 @@ class Work:
             self._ticket = None
 
     def is_completed(self) -> bool:
-        return self._ticket is None
+        """True once the collective has finished on the device (or was waited on / retired):
+        a host-side query, no synchronisation (hang diagnostics)."""
+        if self._ticket is None or not self._comm.handle:
+            return True
+        return self._comm._C.comm_query(self._comm.handle, self._ticket) != 0
+
+    def retire(self):
+        if self._ticket is not None and self._comm.handle:
+            self._comm._C.comm_retire(self._comm.handle, self._ticket)
+        self._ticket = None
+
+    def __del__(self):
+        try:
+            self.retire()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
 
 
 class RcclCommunicator:
@@ -105,7 +127,7 @@ class RcclCommunicator:
         return t
 
     def all_reduce(self, t: torch.Tensor) -> Work:
-        """In-place sum over ranks."""
+        """In-place sum over ranks (any dtype RCCL sums: fp32 / bf16 / fp16 / int64)."""
         return Work(self, int(self._C.comm_all_reduce(self.handle, self._tensor(t))))
 
     def reduce_scatter(self, inp: torch.Tensor, out: torch.Tensor) -> Work:

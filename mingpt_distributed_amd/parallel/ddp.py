@@ -93,6 +93,10 @@ class DataParallelEngine:
         self.done = [False] * len(store.params)
         self.next_launch = 0
         self._hooks = []
+        # (bucket index, elements, work) of the latest synchronised step, kept after finish() for
+        # hang diagnostics (bench.py's watchdog names the first bucket whose collective has not
+        # completed); replaced at the next step's first launch
+        self.inflight: List[tuple] = []
         self.comm = None  # bf16 reduce buffer (same layout as store.grad)
         self.observed: Optional[List[int]] = None  # ready order of the first synchronised backward
         self._recording: Optional[List[int]] = []
@@ -124,11 +128,15 @@ class DataParallelEngine:
 
     # ------------------------------------------------------------------ setup
     def broadcast_params(self, src: int = 0):
-        """Make rank ``src``'s weights authoritative (DDP ctor broadcast, C3)."""
+        """Make the weights of GROUP rank ``src`` of the engine's process group authoritative
+        (DDP ctor broadcast, C3).  Both backends read ``src`` as a group rank: the native
+        communicator's ranks are the group's, and c10d's ``broadcast`` takes a global rank, so
+        it is converted (the two agree on the default group, and differ on a sub-group)."""
         if self.native is not None:
             self.native.broadcast(self.store.master, src).wait()
         else:
-            dist.broadcast(self.store.master, src, group=self.pg)
+            gsrc = dist.get_global_rank(self.pg, src) if self.pg is not None else src
+            dist.broadcast(self.store.master, gsrc, group=self.pg)
         self.store.sync_params_from_master()
 
     @property
@@ -183,10 +191,70 @@ class DataParallelEngine:
         return out
 
     def _launch(self, b: _Bucket):
+        if self.next_launch == 0:
+            self.inflight = []
+        b.work = self._issue(b)
+        self.inflight.append((self.next_launch, b.end - b.start, b.work))
+
+    def _issue(self, b: _Bucket, wire: Optional[torch.Tensor] = None):
+        """Start the bucket's collective on ``wire`` (default: the bucket's slice in the wire
+        dtype, converted now); returns its work handle."""
+        wire = self._wire(b) if wire is None else wire
         if self.native is not None:
-            b.work = self.native.all_reduce(self._wire(b))
-        else:
-            b.work = dist.all_reduce(self._wire(b), op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            return self.native.all_reduce(wire)
+        return dist.all_reduce(wire, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+
+    def time_collectives(self, reps: int = 5) -> List[float]:
+        """Isolated time of every bucket's collective, in launch order (ms per collective, mean
+        of ``reps`` back-to-back calls after a barrier): device time between events on the
+        compute stream on GPUs, host wall time on CPU.  Diagnostics for bench.py, run AFTER the
+        timed steps: it zeroes the wire buffer (sums of zeros stay finite) and leaves no result
+        anyone reads."""
+        if not self.active:
+            return []
+        wire_buf = self.comm if self.comm is not None else self.store.grad
+        wire_buf.zero_()
+        cuda = wire_buf.is_cuda
+        out = []
+        for b in self.buckets:
+            wire = wire_buf[b.start:b.end]
+            self._issue(b, wire).wait()  # warm (first use of this size)
+            dist.barrier(group=self.pg)
+            if cuda:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+                for _ in range(reps):
+                    self._issue(b, wire).wait()
+                ev[1].record()
+                ev[1].synchronize()
+                out.append(ev[0].elapsed_time(ev[1]) / reps)
+            else:
+                import time
+
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    self._issue(b, wire).wait()
+                out.append((time.perf_counter() - t0) * 1e3 / reps)
+        return out
+
+    def bus_bytes(self, b: _Bucket) -> float:
+        """Bytes each rank moves over its links for the bucket's collective (ring accounting,
+        the "bus bandwidth" convention): all-reduce 2 (N-1)/N x bucket bytes."""
+        esz = 2 if self.reduce_dtype == torch.bfloat16 else 4
+        return 2.0 * (self.world - 1) / self.world * (b.end - b.start) * esz
+
+    def incomplete_collectives(self) -> List[tuple]:
+        """(bucket index, elements) of the latest step's collectives that have not completed on
+        the device -- a host-side query, safe from a watchdog thread (diagnostics only)."""
+        out = []
+        for k, n, w in list(self.inflight):
+            try:
+                done = w.is_completed()
+            except Exception:  # noqa: BLE001 -- diagnostics only
+                done = False
+            if not done:
+                out.append((k, n))
+        return out
 
     # ------------------------------------------------------------------ step boundary
     def _wait_all(self):
@@ -270,6 +338,11 @@ class DataParallelEngine:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        for b in self.buckets:  # an unwaited native Work releases its ticket (no stream wait)
+            if b.work is not None and hasattr(b.work, "retire"):
+                b.work.retire()
+            b.work = None
+        self.inflight = []
         for p in self.store.params:
             if getattr(p, "_mg_engine", None) is self:
                 del p._mg_engine

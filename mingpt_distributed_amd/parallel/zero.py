@@ -84,23 +84,27 @@ class ZeroGradEngine(DataParallelEngine):
             self._hook_handle = model.register_forward_pre_hook(self._forward_pre_hook)
 
     # ------------------------------------------------------------------ gradients
-    def _launch(self, b: _Bucket):
-        wire = self._wire(b)
+    def _issue(self, b: _Bucket, wire: Optional[torch.Tensor] = None):
+        wire = self._wire(b) if wire is None else wire
         if self._gloo:
-            b.work = dist.all_reduce(wire, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
-            return
+            return dist.all_reduce(wire, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
         bi = self.buckets.index(b)
         lo, hi = self.own[bi]
         out = wire[lo - b.start:hi - b.start]
         if self.native is not None:
-            b.work = self.native.reduce_scatter(wire, out)
-            return
-        b.work = dist.reduce_scatter_tensor(out, wire, op=dist.ReduceOp.SUM, group=self.pg,
-                                            async_op=True)
+            return self.native.reduce_scatter(wire, out)
+        return dist.reduce_scatter_tensor(out, wire, op=dist.ReduceOp.SUM, group=self.pg,
+                                          async_op=True)
 
     def finish(self):
         self.wait_gathers()  # weights no forward read this step are still owed to the optimizer
         super().finish()
+
+    def bus_bytes(self, b: _Bucket) -> float:
+        """Reduce-scatter: (N-1)/N x bucket bytes per rank (gloo runs an all-reduce: 2x that)."""
+        esz = 2 if self.reduce_dtype == torch.bfloat16 else 4
+        k = 2.0 if self._gloo else 1.0
+        return k * (self.world - 1) / self.world * (b.end - b.start) * esz
 
     def relayout_order(self):
         self.observed = None  # moments are sharded by layout position: keep the layout
@@ -207,8 +211,14 @@ class ZeroAdamW(FusedAdamW):
         pass
 
     def _all_reduce_sumsq(self):
+        """Global squared grad norm = sum of the shards' sums.  Through the engine's native
+        communicator when it has one, so the step's collectives (reduce-scatters, this, the
+        parameter all-gathers) all run in order on ONE comm stream."""
         if self.engine.active:
-            dist.all_reduce(self.norm_buf[:1], group=self.engine.pg)
+            if self.engine.native is not None:
+                self.engine.native.all_reduce(self.norm_buf[:1]).wait()
+            else:
+                dist.all_reduce(self.norm_buf[:1], group=self.engine.pg)
 
     def step(self, grad_scale: float = 1.0, lr: Optional[float] = None):
         s, e = self.store, self.engine
