@@ -32,8 +32,8 @@ struct AttnArgs {
   const uint32_t* dmask;  // dropout keep-bits, row words (attention_train.hip, mask kernel)
   int B, T, H, hd, D;
   float scale_log2;    // log2(e) / sqrt(hd)
-  uint32_t thr;        // 8-bit keep threshold: keep iff random byte >= thr (0 = no dropout)
-  float dscale;        // 1 / (1 - thr/256)
+  uint32_t thr;        // 16-bit keep threshold: keep iff a 16-bit uniform >= thr (0 = no dropout)
+  float dscale;        // 1 / (1 - thr/65536)
   float* dbias;        // bwd key-block mode: += column sums of dK / dV into [D, 3D) (qkv bias grad), or null
 };
 
@@ -44,6 +44,10 @@ inline int nks_for(int hd) {
 }
 
 MG_DEVICE float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }  // v_exp_f32, no denorm fixup
+
+// Bit of score e (= 16 sub + r of a forward lane's 32 scores in a 64-key tile) in its dropout row
+// word: the packed pair j = e >> 1 (P operand word j) at bits 15 - j (low) and 31 - j (high).
+constexpr MG_DEVICE int drop_bit(int e) { return ((e & 1) ? 31 : 15) - (e >> 1); }
 
 // 32-bit avalanche mixer (xorshift-multiply, "lowbias32" constants): a bijection with good
 // avalanche; the attention-dropout bytes are mix32 of distinct counters.

@@ -21,6 +21,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
@@ -115,21 +116,22 @@ MG_DEVICE float block_max(float v, float* red) {
 }
 
 // ---------------------------------------------------------------- residual-stream dropout mask
-// 8-bit decisions (keep iff byte >= thr8, thr8 = round(256 p), scale 256 / (256 - thr8): the same
-// quantised p as the attention dropout).  Element (m, n) of a row-major [M, N] tensor takes byte
-// (n & 3) of the word  fmix32(m * ceil(N / 4) + (n >> 2) + key(seed))  (32-bit index arithmetic:
-// exact below 2^32 words, i.e. 16 G elements per tensor).  One word per 4 consecutive elements:
-// a GEMM epilogue lane holding C[m][n..n+3] draws exactly one, a thread owning 8 consecutive
-// elements two.  The murmur3 finaliser is 2 multiplies per word (a Philox-4x32-10 generator, used
-// in round 1, cost 40 quarter-rate multiplies per 16 decisions and made the standalone dropout-
-// backward kernels RNG-bound).  Counter-based: backward regenerates the mask, nothing is stored.
+// Exact nn.Dropout(p) decisions to 1/65536: keep iff a 16-bit uniform >= thr16 = round(65536 p),
+// scale 65536 / (65536 - thr16) (p = 0.1 -> 0.100006; the 8-bit decisions of rounds 1-3 ran
+// p = 0.1 as 26/256 = 0.1016).  Element (m, n) of a row-major [M, N] tensor takes half (n & 1) of
+// the word  fmix32(m * ceil(N / 2) + (n >> 1) + key(seed))  (32-bit index arithmetic: exact below
+// 2^32 words, i.e. 8 G elements per tensor).  One word per 2 consecutive elements: a GEMM epilogue
+// lane holding C[m][n..n+3] draws two, a thread owning 8 consecutive elements four.  The murmur3
+// finaliser is 2 multiplies per word (a Philox-4x32-10 generator, used in round 1, cost 40
+// quarter-rate multiplies per 16 decisions and made the standalone dropout-backward kernels
+// RNG-bound).  Counter-based: backward regenerates the mask, nothing is stored.
 constexpr uint32_t kRowDropSalt = 0x0d0f0d0fu;
 
-inline uint32_t dropout_threshold8(float p) {
-  const int t = (int)(p * 256.f + 0.5f);
-  return (uint32_t)(t < 0 ? 0 : (t > 256 ? 256 : t));
+inline uint32_t dropout_threshold16(float p) {
+  const double t = (double)p * 65536.0 + 0.5;
+  return (uint32_t)(t < 0.0 ? 0.0 : (t > 65536.0 ? 65536.0 : t));
 }
-inline float dropout_scale8(uint32_t thr8) { return thr8 >= 256 ? 0.f : 256.f / (float)(256 - thr8); }
+inline float dropout_scale16(uint32_t thr16) { return thr16 >= 65536u ? 0.f : 65536.f / (float)(65536u - thr16); }
 
 MG_DEVICE uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;
@@ -145,22 +147,28 @@ MG_DEVICE uint32_t rowdrop_key(uint64_t seed) {
   return fmix32((uint32_t)seed ^ kRowDropSalt) ^ ((uint32_t)(seed >> 32) * 0x9E3779B1u);
 }
 
-// decision word of elements (m, n..n+3), n % 4 == 0
+// decision word of elements (m, n), (m, n + 1), n % 2 == 0
 MG_DEVICE uint32_t rowdrop_word(uint32_t key, long m, int n, int N) {
-  return fmix32((uint32_t)m * (uint32_t)((N + 3) >> 2) + (uint32_t)(n >> 2) + key);
+  return fmix32((uint32_t)m * (uint32_t)((N + 1) >> 1) + (uint32_t)(n >> 1) + key);
 }
 
-// apply the mask to 4 consecutive elements whose 4 decision bytes are `word`
-MG_DEVICE void rowdrop4(float* v, uint32_t word, uint32_t thr8, float scale) {
-#pragma unroll
-  for (int k = 0; k < 4; ++k) v[k] = ((word >> (8 * k)) & 255u) >= thr8 ? v[k] * scale : 0.f;
+// apply the mask to 2 consecutive elements whose decisions are the two halves of `word`
+MG_DEVICE void rowdrop2(float* v, uint32_t word, uint32_t thr16, float scale) {
+  v[0] = (word & 0xffffu) >= thr16 ? v[0] * scale : 0.f;
+  v[1] = (word >> 16) >= thr16 ? v[1] * scale : 0.f;
+}
+
+// 4 consecutive elements (m, n..n+3), n % 4 == 0
+MG_DEVICE void rowdrop4(float* v, uint32_t key, long m, int n, int N, uint32_t thr16, float scale) {
+  rowdrop2(v, rowdrop_word(key, m, n, N), thr16, scale);
+  rowdrop2(v + 2, rowdrop_word(key, m, n + 2, N), thr16, scale);
 }
 
 // 8 consecutive elements (m, n..n+7), n % 8 == 0
-MG_DEVICE void rowdrop8(float (&v)[8], uint64_t seed, long m, int n, int N, uint32_t thr8, float scale) {
+MG_DEVICE void rowdrop8(float (&v)[8], uint64_t seed, long m, int n, int N, uint32_t thr16, float scale) {
   const uint32_t key = rowdrop_key(seed);
-  rowdrop4(v, rowdrop_word(key, m, n, N), thr8, scale);
-  rowdrop4(v + 4, rowdrop_word(key, m, n + 4, N), thr8, scale);
+  rowdrop4(v, key, m, n, N, thr16, scale);
+  rowdrop4(v + 4, key, m, n + 4, N, thr16, scale);
 }
 
 // ---------------------------------------------------------------- GELU (tanh approximation)

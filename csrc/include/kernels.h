@@ -107,8 +107,10 @@ int gemm_get_variant();
 // lse [B*H*T]; dmask: dropout keep-bits generated by attention_fwd when p > 0
 // (attention_dropout_mask_words u32), read by attention_bwd
 size_t attention_dropout_mask_words(int B, int T, int H);
-// 8-bit dropout keep threshold of probability p (keep iff random byte >= thr; 0: no dropout)
+// 16-bit dropout keep threshold of probability p (keep iff a 16-bit uniform >= thr; 0: no dropout)
+// and the matching keep scale 65536 / (65536 - thr)
 int attention_dropout_threshold(float p);
+float attention_dropout_scale(int thr);
 void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, uint32_t* dmask, int B, int T, int H,
                    int hd, float p, uint64_t seed, hipStream_t stream);
 // delta [B*H*T] and dq [attention_bwd_workspace_floats] fp32 are workspaces; writes all three

@@ -44,13 +44,15 @@ namespace {
 #endif
 
 // ------------------------------------------------------------------------------- dropout bits
-// Keep bits (keep iff random byte >= thr) as "row words": word (bh, j, q), j = 2 * tile + h, covers
+// Keep bits (keep iff a 16-bit uniform >= thr) as "row words": word (bh, j, q), j = 2 * tile + h, covers
 // the 32 scores one forward lane holds for query q in 64-key tile `tile`, half h: value
 // e = 16 * sub + r  <->  key 64 * tile + 32 * sub + 4 * h + (r & 3) + 8 * (r >> 2), at bit
-// drop_bit(e) = 8 (e & 3) + (e >> 2).  Stored [bh][j][q]: lanes of consecutive queries read
-// consecutive words in both passes; the forward tests a compile-time bit, the backward a per-lane
-// one.  Randomness: one lowbias32 mix of the word index and seed, then xorshift32 steps -- shifts
-// and xors only (32-bit integer multiplies are quarter rate).
+// drop_bit(e) = (e & 1 ? 31 : 15) - (e >> 1) (attn_common.h): the two scores of packed pair
+// j = e >> 1 (one bf16x2 word of the P operand) sit at bits 15 - j and 31 - j, so one shift and one
+// packed 16-bit arithmetic shift make the pair's 32-bit keep mask (attn_fwd_pipe_kernel).  Stored
+// [bh][j][q]: lanes of consecutive queries read consecutive words in both passes; the backward
+// tests a per-lane bit.  Randomness: one lowbias32 mix of the word index and seed, then xorshift32
+// steps -- shifts and xors only (32-bit integer multiplies are quarter rate), 16 bits a decision.
 //   Tried and removed: the same bits also transposed (32 ballots per wave) into per-register SGPR
 // lane masks so the forward drops a score with ONE v_cndmask_b32: at B = 128 the mask kernel went
 // 106 -> 277 us and the forward gained ~20 us (scalar loads, SGPR spills).
@@ -68,7 +70,8 @@ __global__ __launch_bounds__(256) void attn_dropmask_kernel(uint32_t* __restrict
   const int q = 32 * G + (lane & 31), h = lane >> 5;
   const uint64_t sd = eff_seed(seed, sofs);
   const uint32_t key = (uint32_t)sd ^ mix32((uint32_t)(sd >> 32) + 0x9E3779B9u);
-  const uint32_t kadd = (thr <= 128 ? 128u - thr : 256u - thr) * 0x01010101u;
+  // exact 16-bit decisions (keep iff a 16-bit uniform >= thr, thr = round(65536 p) <= 65535)
+  const uint32_t kadd = (thr <= 0x8000u ? 0x8000u - thr : 0x10000u - thr) * 0x00010001u;
   const int tmax = min(nt - 1, G >> 1);
   for (int t = 0; t <= tmax; ++t) {
     const int j = 2 * t + h;
@@ -77,14 +80,15 @@ __global__ __launch_bounds__(256) void attn_dropmask_kernel(uint32_t* __restrict
       const uint32_t i = (uint32_t)((bh * ntw + j) * T + q);  // the word's index (wraps past 2^32: fine)
       uint32_t x = mix32(i ^ key) | 1u;
 #pragma unroll
-      for (int w = 0; w < 8; ++w) {
+      for (int w = 0; w < 16; ++w) {
         x ^= x << 13;
         x ^= x >> 17;
         x ^= x << 5;
-        // SWAR: bit 7 of byte b <- (byte >= thr); value e = 4 w + b lands at bit 8 b + w
-        const uint32_t y = (x & 0x7f7f7f7fu) + kadd;
-        const uint32_t k7 = (thr <= 128 ? (y | x) : (y & x)) & 0x80808080u;
-        bits |= k7 >> (7 - w);
+        // SWAR over the two 16-bit halves: bit 15 of half k <- (half >= thr); shifted right by w
+        // the two decisions land at bits 15 - w, 31 - w (values e = 2w, 2w + 1): drop_bit(e)
+        const uint32_t y = (x & 0x7fff7fffu) + kadd;
+        const uint32_t k15 = (thr <= 0x8000u ? (y | x) : (y & x)) & 0x80008000u;
+        bits |= k15 >> w;
       }
       dmask[((long)bh * ntw + j) * T + q] = bits;
     }
@@ -173,7 +177,7 @@ MG_DEVICE void fwd_tile(const char* sk, const char* sv, const int (&ko)[NKS], co
     if constexpr (DROP) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int bit = 8 * (r & 3) + (r >> 2) + 4 * sub;  // drop_bit(16 sub + r)
+        const int bit = drop_bit(16 * sub + r);
         const int keep = (int)(kw << (31 - bit)) >> 31;  // sign-extended bit: one v_bfe_i32
         s[sub][r] = __int_as_float(__float_as_int(s[sub][r]) & keep);
       }
@@ -377,6 +381,303 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
   if (two) end_block();
 }
 
+// max of three floats in one v_max3_f32 (inline asm: hipcc canonicalises MFMA results with an
+// extra v_max_f32 x, x before each fmaxf)
+MG_DEVICE float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// keep mask of packed pair j (bf16x2 word j of a lane's P operand): bits 15 - j and 31 - j of the
+// row word, each sign-extended over its 16-bit half (one shift + one v_pk_ashrrev_i16)
+MG_DEVICE uint32_t pair_mask(uint32_t kw, int j) {
+  const s16x2 mk = __builtin_bit_cast(s16x2, kw << j) >> (s16x2){15, 15};
+  return __builtin_bit_cast(uint32_t, mk);
+}
+
+// =============================================================================== pipelined forward
+// Forward for head dims up to 64 (NKS <= 4: one 64-column LDS image), software-pipelined inside
+// each wave so that one tile's softmax VALU issues while the NEXT tile's QK^T MFMAs are in flight:
+//
+//   iteration t:  S(t+1) = (cK(t+1)) Q^T - m   [8 MFMAs, issued first]
+//                 softmax(t): range check (max3), exp2, pack P (bf16 pairs), dropout mask on the
+//                 packed pairs                    [VALU, overlaps the MFMAs above]
+//                 O^T += V^T (Z P)^T, l^T += 1^T P^T [MFMAs; the row sum runs on the matrix pipe]
+//                 stage K(t+2), V(t+1) (register staging), one barrier
+//
+//  * workgroup = 4 waves = 128 queries of one (b, h); 2 workgroups per CU (two waves per SIMD,
+//    from different workgroups, so one wave's softmax and the other's MFMAs interleave too).
+//  * the running max m rides in as the S MFMA's C operand, so p = exp2(S') is one v_exp_f32; m
+//    moves only when a tile's scores leave [-64, 64] (log2 units) -- rare after the first tile of
+//    a block; then o, l and the already-issued next tile are rescaled in place (no recompute).
+//  * the row sum l = sum of the undropped bf16 P is an MFMA against a ones operand (4 per tile)
+//    instead of 32 VALU adds per lane: the matrix pipe has the slack, the vector pipe does not.
+//  * dropout on the packed bf16 P: pair j's keep bits sit at 15 - j and 31 - j of the lane's row
+//    word (drop_bit), so its 32-bit mask is one shift + one v_pk_ashrrev_i16 and the drop one AND
+//    per pair (1.5 VALU per score; was a bit-field extract + AND per fp32 score).
+//  * the causal mask touches only each wave's last (diagonal) tile.
+//  * the workgroups of one (b, h) run 8 apart in the grid (one XCD under round-robin placement:
+//    K / V shared through that XCD's L2), heaviest query block first within the group.
+template <int NKS, bool DROP>
+__global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a) {
+  static_assert(NKS >= 1 && NKS <= 4, "pipelined forward: head dim <= 64");
+  constexpr int NO = (NKS + 1) / 2;  // 32-column O^T accumulator tiles
+  constexpr int TILE = 64 * ROWB;    // one K or V tile (64 keys x 64 columns)
+  constexpr int LM = NKS >= 3;       // row sum on the MFMA pipe (hd 33..64); VALU adds below
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // K0 K1 V0 V1
+  char* const sK = smem;
+  char* const sV = smem + 2 * TILE;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h32 = lane >> 5, l32 = lane & 31;
+  const int nqb = (a.T + 127) / 128;
+  const int npair = (nqb + 1) / 2;
+  const int BH = a.B * a.H;
+  int bh, pr;
+  if ((BH & 7) == 0) {  // the (b, h)'s workgroups 8 apart: one XCD (K / V shared in its L2)
+    const int x = blockIdx.x & 7, rest = blockIdx.x >> 3;
+    pr = rest % npair;
+    bh = (rest / npair) * 8 + x;
+  } else {
+    pr = blockIdx.x % npair;
+    bh = blockIdx.x / npair;
+  }
+  // two query blocks per workgroup, the pr-th heaviest then the pr-th lightest (every workgroup
+  // the same causal work); the K / V tile stream runs on across the seam
+  const int qbA = nqb - 1 - pr, qbB = pr;
+  const int nblk = qbB < qbA ? 2 : 1;
+  const int b = bh / a.H, hh = bh % a.H;
+  const long ld = 3L * a.D;
+  const bf16_t* Qg = a.qkv + (long)b * a.T * ld + hh * a.hd;
+  const bf16_t* Kg = Qg + a.D;
+  const int ntA = (min(a.T, qbA * 128 + 128) + 63) / 64;
+  const int ntB = nblk == 2 ? (min(a.T, qbB * 128 + 128) + 63) / 64 : 0;
+  const int nall = ntA + ntB;  // unified tile stream: A's tiles, then B's
+
+  // ---- K / V staging: thread chunk c -> (row, 16-byte column chunk); per-tile buffer descriptor
+  uint32_t voff[2], sdst[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int idx = threadIdx.x + 256 * c;
+    voff[c] = (uint32_t)(((idx >> 3) * ld + (idx & 7) * 8) * 2);
+    sdst[c] = lds_off(idx >> 3, idx & 7);
+  }
+  const uint64_t kv_bytes = (uint64_t)a.B * a.T * ld * 2;
+  const uint64_t kbase = (uint64_t)((const char*)Kg - (const char*)a.qkv);
+  // unified stream index u -> the (b, h)'s key tile
+  auto src_tile = [&](int u) __attribute__((always_inline)) { return u < ntA ? u : u - ntA; };
+  auto load_k = [&](uint4 (&r)[2], int u) __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t d = kv_rsrc(a.qkv, kv_bytes, kbase + (uint64_t)src_tile(u) * 64 * ld * 2);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) r[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(d, voff[c], 0, 0));
+  };
+  auto load_v = [&](uint4 (&r)[2], int u) __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t d =
+        kv_rsrc(a.qkv, kv_bytes, kbase + (uint64_t)src_tile(u) * 64 * ld * 2 + (uint64_t)a.D * 2);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) r[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(d, voff[c], 0, 0));
+  };
+  auto store_tile = [&](char* dst, const uint4 (&r)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) *reinterpret_cast<uint4*>(dst + sdst[c]) = r[c];
+  };
+
+  // ---- per-lane fragment offsets: K rows l32 (+32 per sub), chunk 2 ks + h32; V^T transposed
+  int ko[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) ko[ks] = lds_off(l32, 2 * ks + h32);
+  const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+  const int ta0 = tr_off(4 * h32 + trq, trc), tb0 = tr_off(8 + 4 * h32 + trq, trc);
+  const int ta1 = tr_off(4 * h32 + trq, 32 + trc), tb1 = tr_off(8 + 4 * h32 + trq, 32 + trc);
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u));
+
+  // ---- prologue staging: K(0), V(0), K(1) loads in flight together
+  {
+    uint4 rk[2], rv[2], rk1[2];
+    load_k(rk, 0);
+    load_v(rv, 0);
+    if (nall > 1) load_k(rk1, 1);
+    store_tile(sK, rk);
+    store_tile(sV, rv);
+    if (nall > 1) store_tile(sK + TILE, rk1);
+  }
+  __syncthreads();
+
+  for (int bi = 0; bi < nblk; ++bi) {
+    const int qb = bi ? qbB : qbA;
+    const int u0 = bi ? ntA : 0;  // stream index of the block's tile 0
+    const int q0 = qb * 128;
+    const int qw = q0 + 32 * w;                                 // this wave's first query
+    const int myq = qw + l32;
+    const int tw = qw < a.T ? min(a.T - 1, qw + 31) / 64 : -1;  // this wave's last (diagonal) tile
+
+    // Q fragments (k-step ks: columns 16 ks + 8 h32 .. +7), pre-scaled into the log2 domain
+    bf16x8 qf[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int d = ks * 16 + 8 * h32;
+      uint4 u = (myq < a.T && d < a.hd) ? ld16(Qg + (long)myq * ld + d) : make_uint4(0, 0, 0, 0);
+      float f[8];
+      unpack8(u, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= a.scale_log2;
+      qf[ks] = __builtin_bit_cast(bf16x8, pack8(f));
+    }
+    f32x16 o[NO], lacc = f32x16{0}, negm = f32x16{0};
+#pragma unroll
+    for (int n = 0; n < NO; ++n) o[n] = f32x16{0};
+    float m = 0.f, lv = 0.f;
+
+    // keep word of tile t (this lane's 32 scores), clamped query row for padding lanes
+    auto row_word = [&](int t) -> uint32_t __attribute__((always_inline)) {
+      return a.dmask[((long)bh * (2 * ((a.T + 63) / 64)) + 2 * t + h32) * a.T + min(myq, a.T - 1)];
+    };
+    // S(t) = (cK(t)) Q^T - m for the wave's 32 queries x the tile's 64 keys (key on the row);
+    // the accumulators are separate named vectors (arrays of them passed around went to scratch)
+    auto scores = [&](f32x16& s0, f32x16& s1, const char* sk) __attribute__((always_inline)) {
+      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_at(sk, ko[0]), qf[0], negm, 0, 0, 0);
+      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_at(sk + 32 * ROWB, ko[0]), qf[0], negm, 0, 0, 0);
+#pragma unroll
+      for (int ks = 1; ks < NKS; ++ks) {
+        s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_at(sk, ko[ks]), qf[ks], s0, 0, 0, 0);
+        s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_row_at(sk + 32 * ROWB, ko[ks]), qf[ks], s1, 0, 0, 0);
+      }
+    };
+    // causal mask of a wave's diagonal tile t: key 64 t + k0 + 4 h32 + (r & 3) + 8 (r >> 2) > query
+    // -> -inf (p = 0).  Applied to S(t) once, right after its MFMAs were issued.
+    auto mask_diag = [&](f32x16& c0, f32x16& c1, int t) __attribute__((always_inline)) {
+      int lim = myq - 64 * t - 4 * h32;
+      asm volatile("" : "+v"(lim));
+      auto mask = [&](f32x16& c, int k0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) c[r] = (k0 + (r & 3) + 8 * (r >> 2) > lim) ? -__builtin_huge_valf() : c[r];
+      };
+      mask(c0, 0);
+      mask(c1, 32);
+    };
+    // p = exp2(S') packed to bf16 pairs (the P^T operand layout of the PV MFMA); rs += sum (hd <= 32)
+    auto expack = [&](const f32x16& c, int st, float& rs) __attribute__((always_inline)) -> bf16x8 {
+      uint32_t u[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p0 = fexp2(c[8 * st + 2 * i]), p1 = fexp2(c[8 * st + 2 * i + 1]);
+        if (!LM) rs += p0 + p1;
+        u[i] = pack2(p0, p1);
+      }
+      return __builtin_bit_cast(bf16x8, make_uint4(u[0], u[1], u[2], u[3]));
+    };
+    // dropped P: pair j's mask = sign-extended bits 15 - j / 31 - j of the row word
+    auto dropped = [&](const bf16x8& pu, int j, uint32_t kw) __attribute__((always_inline)) -> bf16x8 {
+      if constexpr (!DROP) return pu;
+      const uint4 u = __builtin_bit_cast(uint4, pu);
+      return __builtin_bit_cast(bf16x8, make_uint4(u.x & pair_mask(kw, j), u.y & pair_mask(kw, j + 1),
+                                                   u.z & pair_mask(kw, j + 2), u.w & pair_mask(kw, j + 3)));
+    };
+
+    // One tile of one wave: S(t+1) issued first (speculative on the diagonal tile), then S(t)'s
+    // range check, exp2, packing and dropout (VALU beside those MFMAs), the rare rescale, then
+    // O^T += V^T (Z P)^T and l^T += 1^T P^T.
+    auto compute = [&](f32x16& c0, f32x16& c1, f32x16& n0, f32x16& n1, int t, uint32_t kw) __attribute__((always_inline)) {
+      const int u = u0 + t;
+      const char* sv = sV + (u & 1) * TILE;
+      scores(n0, n1, sK + ((u + 1) & 1) * TILE);
+      float mx = max3f(c0[0], c0[1], c0[2]);
+#pragma unroll
+      for (int r = 3; r < 15; r += 2) mx = max3f(mx, c0[r], c0[r + 1]);
+      mx = max3f(mx, c0[15], c1[0]);
+#pragma unroll
+      for (int r = 1; r < 15; r += 2) mx = max3f(mx, c1[r], c1[r + 1]);
+      mx = fmaxf(mx, c1[15]);
+      float rs = 0.f;
+      bf16x8 pu00 = expack(c0, 0, rs), pu01 = expack(c0, 1, rs), pu10 = expack(c1, 0, rs), pu11 = expack(c1, 1, rs);
+      // pinned before the range-check branch, so the exp2 / pack VALU stays beside the S(t+1)
+      // MFMAs (hipcc otherwise sinks it below the branch into the PV block)
+      asm volatile("" ::"v"(pu00), "v"(pu01), "v"(pu10), "v"(pu11));
+      const bool first = t == 0;
+      if (__builtin_expect(__any(mx > 64.f || (first && mx < -64.f)), 0)) {
+        // row max over both halves; a block's first tile may move m down (nothing accumulated yet)
+        const float mr = max_xor32(mx);
+        const float d = first ? mr : fmaxf(mr, 0.f);
+        const float alpha = fexp2(-d);
+#pragma unroll
+        for (int n = 0; n < NO; ++n) o[n] *= alpha;
+        lacc *= alpha;
+        lv *= alpha;
+        m += d;
+        negm = -m;
+        c0 -= d;
+        c1 -= d;
+        n0 -= d;  // S(t+1) was issued against the old m
+        n1 -= d;
+        rs = 0.f;
+        pu00 = expack(c0, 0, rs), pu01 = expack(c0, 1, rs), pu10 = expack(c1, 0, rs), pu11 = expack(c1, 1, rs);
+      }
+      if (!LM) lv += rs;
+      const bf16x8 pd00 = dropped(pu00, 0, kw), pd01 = dropped(pu01, 4, kw), pd10 = dropped(pu10, 8, kw),
+                   pd11 = dropped(pu11, 12, kw);
+      auto pv = [&](const bf16x8& pd, const bf16x8& pu, int rb) __attribute__((always_inline)) {
+#pragma unroll
+        for (int n = 0; n < NO; ++n)
+          o[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              (n & 1) ? lds_tr_at(sv + rb, ta1, tb1) : lds_tr_at(sv + rb, ta0, tb0), pd, o[n], 0, 0, 0);
+        if (LM) lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pu, lacc, 0, 0, 0);
+      };
+      pv(pd00, pu00, 0);  // 16-row aligned LDS row bases: immediates
+      pv(pd01, pu01, 16 * ROWB);
+      pv(pd10, pu10, 32 * ROWB);
+      pv(pd11, pu11, 48 * ROWB);
+      if (t + 1 == tw) mask_diag(n0, n1, t + 1);
+    };
+
+    // block prologue: S(0) from K(u0) (staged), then a barrier before anyone restages that slot
+    uint32_t kw_cur = (DROP && tw >= 0) ? row_word(0) : 0u;
+    f32x16 sA0, sA1, sB0, sB1;
+    if (tw >= 0) {
+      scores(sA0, sA1, sK + (u0 & 1) * TILE);
+      if (tw == 0) mask_diag(sA0, sA1, 0);
+    }
+    __syncthreads();
+
+    // iteration t (stream u = u0 + t): S(t+1) -> n, softmax / PV of tile t from c, stage K(u+2),
+    // V(u+1) into the slots K(u) / V(u-1) held (read before the previous barrier)
+    const int nt = bi ? ntB : ntA;
+    auto iteration = [&](int t, f32x16& c0, f32x16& c1, f32x16& n0, f32x16& n1) __attribute__((always_inline)) {
+      const int u = u0 + t;
+      uint4 rk[2], rv[2];
+      const bool sk2 = u + 2 < nall, sv1 = u + 1 < nall;
+      if (sk2) load_k(rk, u + 2);
+      if (sv1) load_v(rv, u + 1);
+      const uint32_t kw_next = (DROP && t + 1 <= tw) ? row_word(t + 1) : 0u;
+      if (t <= tw) compute(c0, c1, n0, n1, t, kw_cur);
+      kw_cur = kw_next;
+      if (sk2) store_tile(sK + (u & 1) * TILE, rk);
+      if (sv1) store_tile(sV + ((u + 1) & 1) * TILE, rv);
+      __syncthreads();
+    };
+    for (int t = 0; t < nt; t += 2) {
+      iteration(t, sA0, sA1, sB0, sB1);
+      if (t + 1 < nt) iteration(t + 1, sB0, sB1, sA0, sA1);
+    }
+
+    // block epilogue: O = o * dscale / l, lse = m + log2 l (log2 domain)
+    if (myq < a.T) {
+      const float lt = LM ? lacc[0] : sum_xor32(lv);
+      const float inv = (DROP ? a.dscale : 1.f) / lt;
+      if (h32 == 0) a.lse[(long)bh * a.T + myq] = m + log2f(lt);
+      bf16_t* orow = a.out + ((long)b * a.T + myq) * a.D + hh * a.hd;
+#pragma unroll
+      for (int n = 0; n < NO; ++n)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = n * 32 + 8 * g + 4 * h32;
+          if (d < a.hd)
+            *reinterpret_cast<uint2*>(orow + d) = make_uint2(pack2(o[n][4 * g] * inv, o[n][4 * g + 1] * inv),
+                                                             pack2(o[n][4 * g + 2] * inv, o[n][4 * g + 3] * inv));
+        }
+    }
+  }
+}
+
 }  // namespace
 
 namespace mg {
@@ -385,11 +686,13 @@ namespace mg {
 size_t attention_dropout_mask_words(int B, int T, int H) { return (size_t)B * H * T * 2 * ((T + 63) / 64); }
 
 int attention_dropout_threshold(float p) {
-  // 8-bit dropout threshold (as FlashAttention does): effective p = thr / 256
+  // 16-bit dropout threshold: effective p = thr / 65536 (0.1 -> 0.100006)
   if (!(p > 0.f)) return 0;
-  int thr = (int)lrintf(p * 256.f);
-  return thr < 1 ? 1 : (thr > 255 ? 255 : thr);
+  const long thr = lrint((double)p * 65536.0);
+  return (int)(thr < 1 ? 1 : (thr > 65535 ? 65535 : thr));
 }
+
+float attention_dropout_scale(int thr) { return thr ? 65536.f / (65536.f - (float)thr) : 1.f; }
 
 void attention_dropout_mask(uint32_t* dmask, int B, int T, int H, float p, uint64_t seed,
                             hipStream_t stream) {
@@ -406,17 +709,42 @@ static void launch_fwd(const AttnArgs& a, int grid, hipStream_t stream) {
   else attn_fwd_kernel<NKS, false><<<grid, 256, 0, stream>>>(a);
 }
 
+// MINGPT_ATTN_FWD_PIPE=0 keeps the round-3 kernel for hd <= 64 too (A/B only)
+static bool use_pipe() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MINGPT_ATTN_FWD_PIPE");
+    v = e ? atoi(e) : 1;
+  }
+  return v != 0;
+}
+
+template <int NKS>
+static void launch_fwd_pipe(const AttnArgs& a, hipStream_t stream) {
+  const int grid = (cdiv(a.T, 128) + 1) / 2 * a.B * a.H;  // pairs of query blocks
+  if (a.thr) attn_fwd_pipe_kernel<NKS, true><<<grid, 256, 0, stream>>>(a);
+  else attn_fwd_pipe_kernel<NKS, false><<<grid, 256, 0, stream>>>(a);
+}
+
 void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, uint32_t* dmask, int B, int T, int H,
                    int hd, float p, uint64_t seed, hipStream_t stream) {
   AttnArgs a{};
   a.B = B; a.T = T; a.H = H; a.hd = hd; a.D = H * hd;
   a.scale_log2 = 1.4426950408889634f / sqrtf((float)hd);
   a.thr = dmask ? (uint32_t)attention_dropout_threshold(p) : 0u;
-  a.dscale = a.thr ? 256.f / (256.f - (float)a.thr) : 1.f;
+  a.dscale = attention_dropout_scale((int)a.thr);
   a.qkv = qkv; a.out = out; a.lse = lse; a.dmask = dmask;
   if (a.thr) attention_dropout_mask(dmask, B, T, H, p, seed, stream);
   const int nqb = cdiv(T, 128);
   const int grid = (MG_FWD_PAIR ? (nqb + 1) / 2 : nqb) * B * H;  // (pairs of) query blocks
+  if (use_pipe() && nks_for(hd) <= 4) {
+    switch (nks_for(hd)) {
+      case 1: launch_fwd_pipe<1>(a, stream); return;
+      case 2: launch_fwd_pipe<2>(a, stream); return;
+      case 3: launch_fwd_pipe<3>(a, stream); return;
+      default: launch_fwd_pipe<4>(a, stream); return;
+    }
+  }
   switch (nks_for(hd)) {
     case 1: launch_fwd<1>(a, grid, stream); break;
     case 2: launch_fwd<2>(a, grid, stream); break;

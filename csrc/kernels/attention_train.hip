@@ -265,7 +265,7 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
     // this lane's dropout bit inside the keep words (attn_dropmask_kernel layout)
     const int mw_col = (w >> 1) * 2 + ((mykey >> 2) & 1);
     const int mw_el = ((mykey & 32) >> 1) | (mykey & 3) | (((mykey >> 3) & 3) << 2);
-    const int mw_bit = 8 * (mw_el & 3) + (mw_el >> 2);
+    const int mw_bit = drop_bit(mw_el);
     const int t0w = (kb0 / 64) * 2;
 
     f32x16 dk[NO], dv[NO];
@@ -551,323 +551,6 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
   }
 }
 
-// ------------------------------------------------------------ backward, one wave per SIMD
-// Key-block backward at hd = 64 (T a multiple of 256): workgroup = 4 waves = 256 keys of one
-// (b, h), ONE wave per SIMD with the whole 512-register file, each wave 64 keys as two 32-key
-// halves (key on the lane).  Against attn_bwd_kernel (8 waves x 32 keys, 256 registers each):
-//  * K (c-scaled) and V rows of the wave's keys live in registers (no per-tile K reads);
-//  * the Q / dO row fragments (S, dP) and the transposed dO / Q reads (dV, dK) of a 32-query
-//    subtile are read once and feed both halves: half the LDS reads per score;
-//  * per-lane LDS offsets are computed once (room for them in the 512 registers);
-//  * the two halves are independent MFMA chains, so one half's softmax-gradient VALU has the
-//    other half's MFMAs to hide under (one wave per SIMD issues in order: the overlap has to be
-//    in program order, which the half interleave below gives the scheduler).
-// dQ as in key-block mode: dS^T of the 256 keys through LDS, fp32 partial per key block, summed
-// by attn_dq_finalize_kernel.  Dropout: the forward's keep words; both halves of a 64-key tile
-// read the same word of a query (bit + 4 for the second half).
-// dK^T / dV^T accumulate: the accumulators pinned to AGPRs (with the builtin, hipcc shuttles them
-// between AGPRs and VGPRs and spills).  s_nop 1: the B operand may be a just-written VALU result.
-MG_DEVICE void mfma_a32(f32x16& acc, const bf16x8& a, const bf16x8& b) {
-  asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-
-// dropped P and dS / dscale of one 32x32 half in place (S' arrives -inf where the causal mask kills)
-template <bool DROP>
-MG_DEVICE void bwd4_half(f32x16& s, f32x16& dp, const float (&dl)[16], const uint32_t (&mwr)[16], int bit) {
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const float p = fexp2(s[r]);
-    float pd = p;
-    if constexpr (DROP) {
-      int keep;
-      asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(keep) : "v"(mwr[r]), "v"(bit));
-      pd = __int_as_float(__float_as_int(p) & keep);
-    }
-    s[r] = pd;
-    dp[r] = __builtin_fmaf(pd, dp[r], -(p * dl[r]));
-  }
-}
-
-constexpr int kB4Q = 128, kB4K = 256;  // queries per tile, keys per workgroup
-constexpr int B4_OFF_Q = 0, B4_OFF_DO = kB4Q * ROWB, B4_OFF_K = 2 * kB4Q * ROWB;
-constexpr int B4_OFF_DS = B4_OFF_K + kB4K * ROWB;               // dS^T: two [256 keys][64 q] images
-constexpr int B4_OFF_L = B4_OFF_DS + 2 * kB4K * ROWB;           // -lse, delta' [2][128]
-constexpr int B4_OFF_MW = B4_OFF_L + 2 * kB4Q * 4;              // keep words [8][128]
-constexpr int B4_SMEM = B4_OFF_MW + 8 * kB4Q * 4;               // 133 KiB
-
-// One 32-query subtile against the wave's 64 keys.  The causal mask rides in the S init: on the
-// (at most three) subtiles that touch or precede the wave's keys, killed scores start at -inf, so
-// p = exp2(-inf) = 0 and dS = 0; every other subtile starts from -lse alone.  No branch around
-// the accumulating MFMAs: a subtile body per mask case made hipcc copy all 128 dK / dV
-// accumulators between AGPRs at every merge (fully masked subtiles cost nothing in wall time:
-// wave 0 of the same tile has work on all four).
-template <bool DROP>
-MG_DEVICE void bwd4_subtile(const char* smem, int qs, int q0, int k0w, bool masked, int lane, const bf16x8 (&kf)[2][4],
-                            const bf16x8 (&vf)[2][4], f32x16 (&dk)[2][2], f32x16 (&dv)[2][2], const int (&ro)[4],
-                            int ta0, int tb0, int ta1, int tb1, int mw_col, int bit0, int ds_row, int w) {
-  const int h32 = lane >> 5, l32 = lane & 31;
-  const char* sQ = smem + B4_OFF_Q + qs * 32 * ROWB;
-  const char* sdO = smem + B4_OFF_DO + qs * 32 * ROWB;
-  const float* sL = reinterpret_cast<const float*>(smem + B4_OFF_L);
-  const uint32_t* sMW = reinterpret_cast<const uint32_t*>(smem + B4_OFF_MW);
-  float dl[16];
-  uint32_t mwr[16];
-  f32x16 s0, s1, d0 = {0}, d1 = {0};
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {  // row constants of this lane's 16 query rows, 4 per ds_read_b128
-    const int q4 = qs * 32 + 8 * g + 4 * h32;
-    const float4 x = *reinterpret_cast<const float4*>(sL + q4);
-    const float4 y = *reinterpret_cast<const float4*>(sL + kB4Q + q4);
-    s0[4 * g] = x.x; s0[4 * g + 1] = x.y; s0[4 * g + 2] = x.z; s0[4 * g + 3] = x.w;
-    dl[4 * g] = y.x; dl[4 * g + 1] = y.y; dl[4 * g + 2] = y.z; dl[4 * g + 3] = y.w;
-    if constexpr (DROP) {
-      const uint4 m4 = *reinterpret_cast<const uint4*>(sMW + mw_col * kB4Q + q4);
-      mwr[4 * g] = m4.x; mwr[4 * g + 1] = m4.y; mwr[4 * g + 2] = m4.z; mwr[4 * g + 3] = m4.w;
-    } else {
-      mwr[4 * g] = mwr[4 * g + 1] = mwr[4 * g + 2] = mwr[4 * g + 3] = 0u;
-    }
-  }
-  s1 = s0;
-  if (masked) {  // key k0w + 32 a + l32 > query q0 + 4 h32 + (r & 3) + 8 (r >> 2): -inf
-    const int dlt = k0w + l32 - q0 - 4 * h32;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int c = (r & 3) + 8 * (r >> 2);
-      s0[r] = dlt > c ? -__builtin_huge_valf() : s0[r];
-      s1[r] = dlt + 32 > c ? -__builtin_huge_valf() : s1[r];
-    }
-  }
-  // S' = Q (cK)^T - lse, dP~ = dO V^T for both halves: four independent MFMA chains
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const bf16x8 qa = lds_row_at(sQ, ro[ks]);
-    const bf16x8 oa = lds_row_at(sdO, ro[ks]);
-    s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[0][ks], s0, 0, 0, 0);
-    d0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oa, vf[0][ks], d0, 0, 0, 0);
-    s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[1][ks], s1, 0, 0, 0);
-    d1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oa, vf[1][ks], d1, 0, 0, 0);
-  }
-  bwd4_half<DROP>(s0, d0, dl, mwr, bit0);
-  bf16x8 pf0[2], df0[2];
-#pragma unroll
-  for (int st = 0; st < 2; ++st) { pf0[st] = pack_frag(s0, st); df0[st] = pack_frag(d0, st); }
-  bwd4_half<DROP>(s1, d1, dl, mwr, bit0 + 4);
-  bf16x8 pf1[2], df1[2];
-#pragma unroll
-  for (int st = 0; st < 2; ++st) { pf1[st] = pack_frag(s1, st); df1[st] = pack_frag(d1, st); }
-  // dV^T += dO^T P, dK^T += Q^T dS: each transposed dO / Q fragment feeds both halves
-#pragma unroll
-  for (int st = 0; st < 2; ++st) {
-    const int rb = 16 * st * ROWB;
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const bf16x8 to = n ? lds_tr_at(sdO + rb, ta1, tb1) : lds_tr_at(sdO + rb, ta0, tb0);
-      const bf16x8 tq = n ? lds_tr_at(sQ + rb, ta1, tb1) : lds_tr_at(sQ + rb, ta0, tb0);
-      mfma_a32(dv[0][n], to, pf0[st]);
-      mfma_a32(dv[1][n], to, pf1[st]);
-      mfma_a32(dk[0][n], tq, df0[st]);
-      mfma_a32(dk[1][n], tq, df1[st]);
-    }
-  }
-  // dS^T (scaled by 1/dscale) rows = keys: image (qs >> 1), columns (qs & 1) * 32 + 8 g + 4 h32
-  char* img = const_cast<char*>(smem) + B4_OFF_DS + (qs >> 1) * kB4K * ROWB;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int qc = (qs & 1) * 32 + 8 * g + 4 * h32;
-    const int o = lds_off(ds_row, qc >> 3) + (qc & 7) * 2;
-    const uint4 a0 = __builtin_bit_cast(uint4, df0[g >> 1]);
-    const uint4 a1 = __builtin_bit_cast(uint4, df1[g >> 1]);
-    *reinterpret_cast<uint2*>(img + o) = (g & 1) ? make_uint2(a0.z, a0.w) : make_uint2(a0.x, a0.y);
-    *reinterpret_cast<uint2*>(img + o + 32 * ROWB) = (g & 1) ? make_uint2(a1.z, a1.w) : make_uint2(a1.x, a1.y);
-  }
-}
-
-template <bool DROP>
-__global__ __launch_bounds__(256, 1) void attn_bwd4_kernel(const AttnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int h32 = lane >> 5, l32 = lane & 31;
-  const int BH = a.B * a.H;
-  const int kb = blockIdx.x / BH, bh = blockIdx.x % BH;  // key block 0 (the heaviest) first
-  const int b = bh / a.H, hh = bh % a.H;
-  const long ld = 3L * a.D;
-  const bf16_t* Qg = a.qkv + (long)b * a.T * ld + hh * 64;
-  const bf16_t* Kg = Qg + a.D;
-  const bf16_t* Vg = Qg + 2 * a.D;
-  const bf16_t* dOg = a.dout + (long)b * a.T * a.D + hh * 64;
-  const float* lseg = a.lse + (long)bh * a.T;
-  const float* dlg = a.delta + (long)bh * a.T;
-  const int kb0 = kb * kB4K, k0w = kb0 + 64 * w;
-  const int ntw = 2 * (a.T / 64), t0w = (kb0 / 64) * 2;
-  const int nqt = a.T / kB4Q, qt0 = kb0 / kB4Q;
-  const float ddl = 1.f / a.dscale;
-  char* sK = smem + B4_OFF_K;
-
-  using stq = Stager<kB4Q, 1, 256>;
-  using stk = Stager<kB4K, 1, 256>;
-  {  // K <- c K into LDS (all 256 keys: the dQ operand)
-    uint4 rk[stk::N];
-    stk::load(rk, Kg, ld, kb0, a.T, 64);
-#pragma unroll
-    for (int i = 0; i < stk::N; ++i) {
-      float f[8];
-      unpack8(rk[i], f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] *= a.scale_log2;
-      rk[i] = pack8(f);
-    }
-    stk::store(sK, rk);
-  }
-  bf16x8 vf[2][4], kf[2][4];
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-      vf[hf][ks] = __builtin_bit_cast(bf16x8, ld16(Vg + (long)(k0w + 32 * hf + l32) * ld + ks * 16 + 8 * h32));
-
-  // per-lane constants
-  int ro[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) ro[ks] = lds_off(l32, (2 * ks + h32) & 7);
-  const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-  const int ta0 = tr_off(4 * h32 + trq, trc), tb0 = tr_off(8 + 4 * h32 + trq, trc);
-  const int ta1 = tr_off(4 * h32 + trq, 32 + trc), tb1 = tr_off(8 + 4 * h32 + trq, 32 + trc);
-  const int mw_col = 2 * w + ((l32 >> 2) & 1);
-  const int bit0 = 8 * (l32 & 3) + ((l32 >> 3) & 3);
-  const int ds_row = 64 * w + l32;  // dS^T image row of this lane's first-half key
-
-  f32x16 dk[2][2], dv[2][2];
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-    for (int n = 0; n < 2; ++n) { dk[hf][n] = f32x16{0}; dv[hf][n] = f32x16{0}; }
-
-  uint4 rq[stq::N], rd[stq::N];
-  uint32_t oq[stq::N], od[stq::N];
-  stq::offsets(oq, ld);
-  stq::offsets(od, a.D);
-  const uint64_t q_total = (uint64_t)a.B * a.T * ld * 2, do_total = (uint64_t)a.B * a.T * a.D * 2;
-  const uint64_t q_org = (uint64_t)((const char*)Qg - (const char*)a.qkv);
-  const uint64_t do_org = (uint64_t)((const char*)dOg - (const char*)a.dout);
-  float rl = 0.f;
-  uint32_t rmw[4] = {~0u, ~0u, ~0u, ~0u};
-  auto issue = [&](int qt) {
-    stq::load_buf(rq, a.qkv, q_total, q_org + (uint64_t)qt * kB4Q * ld * 2, oq);
-    stq::load_buf(rd, a.dout, do_total, do_org + (uint64_t)qt * kB4Q * a.D * 2, od);
-    const int t = threadIdx.x;
-    const int q = qt * kB4Q + (t & (kB4Q - 1));
-    rl = t < kB4Q ? -lseg[q] : dlg[q] * ddl;  // -lse: the S init (K holds c K)
-    if constexpr (DROP) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {  // word j = u / 128 of query row q -> sMW[u]
-        const int u = t + 256 * i;
-        rmw[i] = a.dmask[((long)bh * ntw + t0w + (u >> 7)) * a.T + qt * kB4Q + (u & (kB4Q - 1))];
-      }
-    }
-  };
-  auto commit = [&]() {
-    stq::store(smem + B4_OFF_Q, rq);
-    stq::store(smem + B4_OFF_DO, rd);
-    reinterpret_cast<float*>(smem + B4_OFF_L)[threadIdx.x] = rl;
-    if constexpr (DROP) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) reinterpret_cast<uint32_t*>(smem + B4_OFF_MW)[threadIdx.x + 256 * i] = rmw[i];
-    }
-  };
-  issue(qt0);
-  commit();
-  __syncthreads();  // K, first Q / dO tile
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) kf[hf][ks] = lds_row_at(sK + (64 * w + 32 * hf) * ROWB, ro[ks]);
-
-  const float dq_scale = 0.6931471805599453f * a.dscale;
-  (void)dq_scale;
-  for (int qt = qt0; qt < nqt; ++qt) {
-    const bool more = qt + 1 < nqt;
-    if (more) issue(qt + 1);
-#pragma unroll 1
-    for (int qs = 0; qs < 4; ++qs) {
-      const int q0 = qt * kB4Q + qs * 32;
-      bwd4_subtile<DROP>(smem, qs, q0, k0w, k0w + 63 > q0, lane, kf, vf, dk, dv, ro, ta0, tb0, ta1, tb1, mw_col,
-                         bit0, ds_row, w);
-    }
-    __syncthreads();  // dS^T of all 256 keys in LDS
-    // dQ[128 q][64] = dS[128 q][256 keys] (c K)[256 keys][64]: 8 32x32 tiles, two per wave
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int tt = w + 4 * i, qs = tt >> 1, n = tt & 1;
-      const int qcol = (qs & 1) * 32 + trc;
-      const int da = tr_off(8 * h32 + trq, qcol), db = tr_off(8 * h32 + 4 + trq, qcol);
-      const int ka = tr_off(8 * h32 + trq, n * 32 + trc), kb4 = tr_off(8 * h32 + 4 + trq, n * 32 + trc);
-      const char* sdSh = smem + B4_OFF_DS + (qs >> 1) * kB4K * ROWB;
-      f32x16 dq = {0};
-#pragma unroll
-      for (int kk = 0; kk < kB4K / 16; ++kk)
-        dq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_at(sdSh + kk * 16 * ROWB, da, db),
-                                                     lds_tr_at(sK + kk * 16 * ROWB, ka, kb4), dq, 0, 0, 0);
-      // fp32 partial of key block kb: rows q0 + (r & 3) + 8 (r >> 2), column n * 32 + l32
-      const int q0 = qt * kB4Q + qs * 32 + 4 * h32;
-      float* dqb = a.dq + (long)kb * a.dq_part + ((long)b * a.T + q0) * a.D + hh * 64 + n * 32 + l32;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dqb[(long)((r & 3) + 8 * (r >> 2)) * a.D] = dq[r];
-    }
-    if (more) commit();
-    __syncthreads();
-  }
-
-  // dK (scaled), dV (dropout keep scale folded) -> dqkv K / V slots; lane = key,
-  // d = n*32 + 8*(r>>2) + 4*h32 + (r&3)
-  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // the last asm MFMA's results (hipcc cannot see them)
-  const float sc = a.scale_log2 * 0.6931471805599453f * a.dscale;  // dscale / sqrt(hd)
-  const float vs = a.thr ? a.dscale : 1.f;
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-    bf16_t* krow = a.dqkv + ((long)b * a.T + k0w + 32 * hf + l32) * ld + a.D + hh * 64;
-    bf16_t* vrow = krow + a.D;
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = n * 32 + 8 * g + 4 * h32;
-        *reinterpret_cast<uint2*>(krow + d) = make_uint2(pack2(dk[hf][n][4 * g] * sc, dk[hf][n][4 * g + 1] * sc),
-                                                         pack2(dk[hf][n][4 * g + 2] * sc, dk[hf][n][4 * g + 3] * sc));
-        *reinterpret_cast<uint2*>(vrow + d) = make_uint2(pack2(dv[hf][n][4 * g] * vs, dv[hf][n][4 * g + 1] * vs),
-                                                         pack2(dv[hf][n][4 * g + 2] * vs, dv[hf][n][4 * g + 3] * vs));
-      }
-  }
-  if (a.dbias) {
-    // qkv bias gradient, K and V columns: both halves and the 32 lanes of a half summed in
-    // registers, the 4 waves through LDS (every read of the last tile is behind its barrier), one
-    // fp32 atomic per column
-    constexpr int NV = 64;  // this lane's dK then dV values (2 x 16 x NO)
-    float v[NV];
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        v[n * 16 + r] = (dk[0][n][r] + dk[1][n][r]) * sc;
-        v[32 + n * 16 + r] = (dv[0][n][r] + dv[1][n][r]) * vs;
-      }
-    tr_reduce32<16, NV, NV>(v, lane);
-    float* red = reinterpret_cast<float*>(smem);  // [4][2][64]
-#pragma unroll
-    for (int j = 0; j < 2; ++j) red[(w * 2 + j) * 64 + lane] = v[j];
-    __syncthreads();
-    if (threadIdx.x < 128) {
-      const int t = threadIdx.x, ln = t & 63, j = t >> 6;
-      float s = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < 4; ++ww) s += red[(ww * 2 + j) * 64 + ln];
-      const int idx = 2 * (ln & 31) + j;  // value index (tr_reduce32)
-      const int tk = idx / 32, n = (idx % 32) / 16, r = idx % 16;
-      const int d = n * 32 + 8 * (r >> 2) + 4 * (ln >> 5) + (r & 3);
-      atomicAdd(a.dbias + (1 + tk) * a.D + hh * 64 + d, s);
-    }
-  }
-}
-
 // partial mode: dqkv Q slot = bf16(scale * sum of the dQ partials of key blocks kb <= t / KB)
 __global__ __launch_bounds__(256) void attn_dq_finalize_kernel(const float* __restrict__ dq,
                                                                bf16_t* __restrict__ dqkv, int rows,
@@ -932,41 +615,17 @@ int bwd_keys_per_block(int hd) { return nks_for_bwd(hd) > 4 ? 128 : 256; }
 // sweeping its key blocks, dQ summed in place) even where B*H fills the chip in whole rounds --
 // the in-place read-add-store of dQ costs the persistent kernel more than the finalize pass.
 // Persistent mode is used when there is a single key block (no partial sum to form).
-int g_bwd_mode = -1;  // 0 auto, 1 force persistent, 2 force key-block, 3 force bwd4 (tests, MINGPT_ATTN_BWD_MODE)
+// (The one-wave-per-SIMD key-block backward of round 3, 4 waves x 64 keys with the whole register
+// file, measured 1,453 vs 1,251 us at B = 128 and was removed: PERF.md, round 3.)
+int g_bwd_mode = -1;  // 0 auto, 1 force persistent, 2 force key-block (tests, MINGPT_ATTN_BWD_MODE)
 
 bool bwd_persistent(int T, int hd) {
   if (g_bwd_mode < 0) {
     const char* e = getenv("MINGPT_ATTN_BWD_MODE");
     g_bwd_mode = e ? atoi(e) : 0;
   }
-  if (g_bwd_mode) return g_bwd_mode == 1;  // 3 (bwd4) is a key-block schedule too
+  if (g_bwd_mode) return g_bwd_mode == 1;
   return T <= bwd_keys_per_block(hd);
-}
-
-// attn_bwd4_kernel where it applies (hd = 64, T a multiple of its 256-key block, more than one key
-// block): in mode 3 and with MINGPT_ATTN_BWD4=1; off by default -- measured slower than
-// attn_bwd_kernel at the GPT-2 shape (B = 128: 1,453 vs 1,251 us; PERF.md, round 3)
-bool use_bwd4(int T, int hd) {
-  static int env = -1;
-  if (env < 0) {
-    const char* e = getenv("MINGPT_ATTN_BWD4");
-    env = e ? atoi(e) : 0;
-  }
-  if (hd != 64 || T % kB4K != 0 || T <= kB4K) return false;
-  if (g_bwd_mode == 3) return true;
-  return g_bwd_mode == 0 && env != 0 && !bwd_persistent(T, hd);
-}
-
-void launch_bwd4(const AttnArgs& a, hipStream_t stream) {
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)attn_bwd4_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, B4_SMEM);
-    hipFuncSetAttribute((const void*)attn_bwd4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, B4_SMEM);
-    attr = true;
-  }
-  const int grid = a.B * a.H * (a.T / kB4K);
-  if (a.thr) attn_bwd4_kernel<true><<<grid, 256, B4_SMEM, stream>>>(a);
-  else attn_bwd4_kernel<false><<<grid, 256, B4_SMEM, stream>>>(a);
 }
 
 template <int NKS, int KW>
@@ -998,7 +657,7 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
   a.B = B; a.T = T; a.H = H; a.hd = hd; a.D = H * hd;
   a.scale_log2 = 1.4426950408889634f / sqrtf((float)hd);
   a.thr = dmask ? (uint32_t)attention_dropout_threshold(p) : 0u;
-  a.dscale = a.thr ? 256.f / (256.f - (float)a.thr) : 1.f;
+  a.dscale = attention_dropout_scale((int)a.thr);
   a.qkv = qkv; a.out = dqkv; a.lse = const_cast<float*>(lse); a.dout = dout; a.delta = delta;
   a.dq = dq; a.dqkv = dqkv; a.dmask = dmask;
   const bool persistent = bwd_persistent(T, hd);
@@ -1015,17 +674,13 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
   const long nthreads = (long)B * T * H << lg;
   if (!delta_ready)
     attn_bwd_pre_kernel<<<(unsigned)cdiv(nthreads, 256), 256, 0, stream>>>(dout, out, delta, B * T, T, H, hd, lg);
-  if (!persistent && use_bwd4(T, hd)) {
-    launch_bwd4(a, stream);
-  } else {
-    switch (nks_for(hd)) {
-      case 1: launch_bwd<1, 8>(a, stream); break;
-      case 2: launch_bwd<2, 8>(a, stream); break;
-      case 3: launch_bwd<3, 8>(a, stream); break;
-      case 4: launch_bwd<4, 8>(a, stream); break;
-      case 6: launch_bwd<6, 4>(a, stream); break;
-      default: launch_bwd<8, 4>(a, stream); break;
-    }
+  switch (nks_for(hd)) {
+    case 1: launch_bwd<1, 8>(a, stream); break;
+    case 2: launch_bwd<2, 8>(a, stream); break;
+    case 3: launch_bwd<3, 8>(a, stream); break;
+    case 4: launch_bwd<4, 8>(a, stream); break;
+    case 6: launch_bwd<6, 4>(a, stream); break;
+    default: launch_bwd<8, 4>(a, stream); break;
   }
   if (!persistent) {
     const long n8 = (long)B * T * (H * hd / 8);

@@ -236,9 +236,9 @@ void bias_act_fwd(const bf16_t* x, const bf16_t* b, bf16_t* pre, bf16_t* y, long
 void bias_dropout_residual(const bf16_t* x, const bf16_t* b, const bf16_t* r, bf16_t* y, long M,
                            int N, float p, uint64_t seed, hipStream_t stream) {
   const long n8 = M * N / 8;
-  const uint32_t thr = dropout_threshold8(p);
+  const uint32_t thr = dropout_threshold16(p);
   bias_drop_resid_kernel<<<grid_for(n8), 256, 0, stream>>>(x, b, r, y, n8, N, seed, thr,
-                                                           dropout_scale8(thr), thr > 0,
+                                                           dropout_scale16(thr), thr > 0,
                                                            graph_seed_ofs());
 }
 
@@ -248,9 +248,9 @@ void gelu_bwd(const bf16_t* dy, const bf16_t* pre, bf16_t* dx, long n, hipStream
 
 void dropout_bwd(const bf16_t* dy, bf16_t* dx, long M, int N, float p, uint64_t seed,
                  hipStream_t stream) {
-  const uint32_t thr = dropout_threshold8(p);
+  const uint32_t thr = dropout_threshold16(p);
   const long n8 = M * N / 8;
-  dropout_bwd_kernel<<<grid_for(n8), 256, 0, stream>>>(dy, dx, n8, N, seed, thr, dropout_scale8(thr),
+  dropout_bwd_kernel<<<grid_for(n8), 256, 0, stream>>>(dy, dx, n8, N, seed, thr, dropout_scale16(thr),
                                                        graph_seed_ofs());
 }
 
@@ -266,15 +266,15 @@ static dim3 bias_grid(long M, int N, int cvb) {
 
 void dropout_bias_grad(const bf16_t* dy, bf16_t* dx, float* db, long M, int N, float p, uint64_t seed,
                        hipStream_t stream) {
-  const uint32_t thr = dropout_threshold8(p);
+  const uint32_t thr = dropout_threshold16(p);
   const int cvb = bias_cvb(N);
   const dim3 grid = bias_grid(M, N, cvb);
   if (cvb == 32)
     dropout_bias_grad_kernel<32><<<grid, 256, 0, stream>>>(dy, dx, db, (int)M, N, seed, thr,
-                                                           dropout_scale8(thr), graph_seed_ofs());
+                                                           dropout_scale16(thr), graph_seed_ofs());
   else
     dropout_bias_grad_kernel<64><<<grid, 256, 0, stream>>>(dy, dx, db, (int)M, N, seed, thr,
-                                                           dropout_scale8(thr), graph_seed_ofs());
+                                                           dropout_scale16(thr), graph_seed_ofs());
 }
 
 void transpose(const bf16_t* src, bf16_t* dst, int R, int C, int ldd, hipStream_t stream) {

@@ -135,17 +135,17 @@ void embedding_fwd(const int64_t* idx, const bf16_t* wte, const bf16_t* wpe, bf1
                    int T, int D, int V, float p, uint64_t seed, hipStream_t stream, const int* pos_dev,
                    const unsigned long long* am_part, int am_groups, int64_t* tok, int64_t* seq,
                    long seq_ld) {
-  const uint32_t thr = dropout_threshold8(p);  // the 8-bit residual-stream mask (common.h)
+  const uint32_t thr = dropout_threshold16(p);  // the residual-stream mask (common.h)
   emb_fwd_kernel<<<cdiv(M, 4), 256, 0, stream>>>(idx, wte, wpe, out, M, T, D, V, debug_err_word(), seed, thr,
-                                                 dropout_scale8(thr), p > 0.f,
+                                                 dropout_scale16(thr), p > 0.f,
                                                  graph_seed_ofs(), pos_dev, am_part, am_groups, tok, seq,
                                                  seq_ld);
 }
 
 void embedding_bwd(const int64_t* idx, const bf16_t* dout, float* dwte, float* dwpe, int M, int T,
                    int D, int V, float p, uint64_t seed, hipStream_t stream) {
-  const uint32_t thr = dropout_threshold8(p);
-  const float scale = dropout_scale8(thr);
+  const uint32_t thr = dropout_threshold16(p);
+  const float scale = dropout_scale16(thr);
   if (dwte)
     emb_bwd_wte_kernel<<<cdiv(M, 4), 256, 0, stream>>>(idx, dout, dwte, M, D, V, debug_err_word(), seed, thr, scale,
                                                        p > 0.f, graph_seed_ofs());

@@ -488,7 +488,7 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
               make_uint2(pack2(g0.x, g0.y), pack2(g1.x, g1.y));
         }
         if constexpr (EPI == 3) {
-          if (args.thr) rowdrop4(v, rowdrop_word(dkey, m, n, args.N), args.thr, args.scale);  // common.h
+          if (args.thr) rowdrop4(v, dkey, m, n, args.N, args.thr, args.scale);  // common.h
         }
         if constexpr (F32)
           *reinterpret_cast<float4*>(row + col * 4) = make_float4(v[0], v[1], v[2], v[3]);
@@ -639,7 +639,7 @@ MG_DEVICE void epilogue(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int 
           *reinterpret_cast<uint2*>(args.aux + off) = make_uint2(pack2(gd[0], gd[1]), pack2(gd[2], gd[3]));
         }
         if constexpr (EPI == 3) {
-          if (args.thr) rowdrop4(v, rowdrop_word(dkey, m, n, args.N), args.thr, args.scale);  // common.h
+          if (args.thr) rowdrop4(v, dkey, m, n, args.N, args.thr, args.scale);  // common.h
           v[0] += bf2f(side[j].x & 0xffffu); v[1] += bf2f(side[j].x >> 16);
           v[2] += bf2f(side[j].y & 0xffffu); v[3] += bf2f(side[j].y >> 16);
         }
@@ -1384,8 +1384,8 @@ void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long l
   a.A = A; a.B = B; a.C = C; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.M = M; a.N = N; a.K = K; a.a_ext = a_ext; a.b_ext = b_ext; a.ka = ka; a.kb = kb;
   a.bias = bias; a.aux = aux; a.resid = resid; a.seed = seed; a.sofs = graph_seed_ofs();
-  a.thr = dropout_threshold8(p);  // EPI 3 residual dropout: 8-bit row-block mask (common.h)
-  a.scale = dropout_scale8(a.thr);
+  a.thr = dropout_threshold16(p);  // EPI 3 residual dropout: 16-bit row-block mask (common.h)
+  a.scale = dropout_scale16(a.thr);
   a.tiles_m = a.tiles_n = a.splits = 1;
   a.kchunk = K;
   a.dbg = g_dbg;

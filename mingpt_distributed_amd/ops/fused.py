@@ -7,14 +7,11 @@ embedding and one for final-LN + LM head + cross-entropy.  Every norm, attention
 elementwise op and every GEMM -- the fused-epilogue ones (bias+GELU, bias+dropout+residual,
 GELU', the weight gradients with their fp32 accumulation), the plain ones of a block (qkv
 projection, the three data gradients) and the LM head's forward, weight and data gradients -- is
-a hand-written HIP kernel: no library GEMM runs in the default step.  ``MINGPT_LMHEAD_BLAS=1``
-puts the LM head's forward on hipBLASLt (through torch.mm), which is 1.2 % of the B=64 step
-faster there (K = 768 with 6.6 GB of logits written; PERF.md), as the project brief allows for
-plain library GEMMs; ``MINGPT_QKV_BLAS=1 MINGPT_DGRAD_BLAS=1 MINGPT_LMHEAD_DGRAD_BLAS=1`` restores
-round 1's library routing of the other plain GEMMs (equal in the step once the W4 main loop
-improved).  Weight gradients are accumulated in fp32 straight into ``param.main_grad`` (see
-``grads.py``) so the data-parallel engine can all-reduce a bucket the moment its last gradient
-lands.
+a hand-written HIP kernel (``gemm.hip`` through :mod:`.gemm`): there is one backend, no library
+GEMM and no runtime switch to one (hipBLASLt comparisons live in ``bench/`` microbenchmarks only:
+``bench/gemm_blas_shapes.py``, ``bench/bench_wgrad_blas.py``).  Weight gradients are accumulated
+in fp32 straight into ``param.main_grad`` (see ``grads.py``) so the data-parallel engine can
+all-reduce a bucket the moment its last gradient lands.
 
 Reference anchors: block structure ``/root/reference/mingpt/model.py:171-189`` (with D4/D5/D6
 fixed), embedding ``model.py:193-231``, head + loss ``model.py:309-320``.
@@ -41,17 +38,6 @@ def _bf16(t: torch.Tensor) -> torch.Tensor:
 
 # ------------------------------------------------------------------------------------ embedding
 
-# Plain GEMMs of the block (no fused epilogue): the three epilogue-free data gradients (qkv,
-# attention projection, MLP fc) and the qkv projection (bias only) run on gemm.hip by default.
-# Round 1 routed them to hipBLASLt (+1.7 % then); after the W4 main-loop work the HIP kernels are
-# as fast or faster on these shapes (bench/gemm_blas_shapes.py: qkv 220 vs 248 us, fc dgrad 240
-# vs 266, qkv dgrad 178 vs 192, proj dgrad 80 vs 82) and the step A/B is equal (999.5k both,
-# profiles/round2_gemm_routing_ab.txt).  MINGPT_{DGRAD,QKV}_BLAS=1 restores the library routing.
-# The weight gradients stay on gemm.hip (fp32 accumulate; the fp32-out library GEMM + add was
-# 13 % slower per step).
-_DGRAD_BLAS = os.environ.get("MINGPT_DGRAD_BLAS", "0") == "1"
-_WGRAD_BLAS = os.environ.get("MINGPT_WGRAD_BLAS", "0") == "1"
-_QKV_BLAS = os.environ.get("MINGPT_QKV_BLAS", "0") == "1"
 # The MLP fc bias gradient summed inside the fc2 data-gradient GEMM's staged epilogue (one add per
 # stored element, one atomic per tile column) instead of a separate 400 MB column-sum pass over
 # dpre.  MINGPT_FC_DBIAS_FUSED=0 restores the separate bias_grad kernel.
@@ -68,29 +54,14 @@ _QKV_DBIAS_FUSED = os.environ.get("MINGPT_QKV_DBIAS_FUSED", "1") == "1"
 _DELTA_FUSED = os.environ.get("MINGPT_DELTA_FUSED", "0") == "1"
 
 
-# Library calls cost more host time per launch than the extension's; small models (gpt-mini:
-# M = 8192, K = 192) are launch-bound and ran 15 % slower through hipBLASLt (one-box A/B), so
-# only GEMMs of at least this many multiply-adds take the library path.
-_BLAS_MIN_MNK = 5e9
-
-
-def _big(m, n, k):
-    return float(m) * n * k >= _BLAS_MIN_MNK
-
-
 def _dgrad(dy, w):
-    """dX = dY @ W for a plain (epilogue-free) data gradient."""
-    if _DGRAD_BLAS and _big(dy.shape[0], w.shape[1], w.shape[0]):
-        return torch.mm(dy, w)
+    """dX = dY @ W for a plain (epilogue-free) data gradient (gemm.hip, weight read in place)."""
     return G.gemm_dgrad(dy, w)
 
 
 def _wgrad(dy, x, main_grad):
-    """main_grad += dY^T @ X (fp32)."""
-    if _WGRAD_BLAS:
-        main_grad.add_(torch.mm(dy.t(), x, out_dtype=torch.float32))
-    else:
-        G.gemm_tn_acc(dy, x, main_grad)
+    """main_grad += dY^T @ X (gemm.hip split-K, fp32 accumulate in the epilogue)."""
+    G.gemm_tn_acc(dy, x, main_grad)
 
 
 class _EngineFn(torch.autograd.Function):
@@ -142,10 +113,7 @@ class TransformerBlockFn(_EngineFn):
         seeds = (new_seed() if p_attn > 0 else 0, new_seed() if p_resid > 0 else 0,
                  new_seed() if p_resid > 0 else 0)
         h, mean1, rstd1 = C.layernorm_fwd(x, ln1w, ln1b, eps)
-        if _QKV_BLAS and _big(h.shape[0], wqkv.shape[0], h.shape[1]):
-            qkv = torch.addmm(bqkv, h, wqkv.t())
-        else:
-            qkv = G.gemm_nt(h, wqkv, bias=bqkv, epi="bias")
+        qkv = G.gemm_nt(h, wqkv, bias=bqkv, epi="bias")
         y, lse, amask = C.attention_fwd(qkv, B, T, H, float(p_attn), seeds[0])
         x1 = G.gemm_nt(y, wo, bias=bo, epi="resid", resid=x, p=p_resid, seed=seeds[1])
         h2, mean2, rstd2 = C.layernorm_fwd(x1, ln2w, ln2b, eps)
@@ -191,7 +159,7 @@ class TransformerBlockFn(_EngineFn):
         _wgrad(dz, y, g[id(wo)][0])
         hd = wo.shape[0] // H
         delta = None
-        if _DELTA_FUSED and hd in (8, 16, 32, 64) and not (_DGRAD_BLAS and _big(dz.shape[0], wo.shape[1], wo.shape[0])):
+        if _DELTA_FUSED and hd in (8, 16, 32, 64):
             # the attention backward's rowsum(dO * O) in the dO GEMM's epilogue (no separate pass)
             delta = torch.empty(B * H * T, dtype=torch.float32, device=dz.device)
             dy = G.gemm_nn(dz, wo, epi="delta", aux=y, delta=(delta, T, H, hd))
@@ -212,28 +180,12 @@ class TransformerBlockFn(_EngineFn):
 
 
 # ------------------------------------------------------------------------------------ head + loss
-# The LM head's forward carries no epilogue (plain [M, 768] x [768, 50304], K = 768, 6.6 GB of
-# logits written): gemm.hip's W4 kernel by default (5.0 ms per call at B = 64), hipBLASLt via
-# torch.mm against a zero-padded weight copy with MINGPT_LMHEAD_BLAS=1 (4.1 ms, +1.2 % step).  Its
-# data gradient ([M, 50304] x [50304, 768], K = 50304) runs on gemm.hip (the 128x96-wave W4 tile:
-# 3.75 vs 3.81 ms), the weight gradient too (fp32 accumulate into main_grad).
-# MINGPT_LMHEAD_DGRAD_BLAS=1 (with MINGPT_LMHEAD_BLAS=1) puts the data gradient on the library.
-_LMHEAD_BLAS = os.environ.get("MINGPT_LMHEAD_BLAS", "0") == "1"
-_LMHEAD_DGRAD_BLAS = os.environ.get("MINGPT_LMHEAD_DGRAD_BLAS", "0") == "1"
-# Training cross-entropy in one pass over the logits (xent.hip xent_fused: loss and
-# dlogits = (softmax - onehot) / n_valid written in forward, grad_out applied in backward).
-# MINGPT_XENT_FUSED=0 keeps the two-pass fwd / bwd kernels.
+# The LM head's forward ([M, 768] x [768, 50304], K = 768, 13 GB of logits at B = 128), data
+# gradient ([M, 50304] x [50304, 768]: the 128x96-wave W4 tile) and weight gradient (fp32
+# accumulate into main_grad) all run on gemm.hip.  Training cross-entropy in one pass over the
+# logits (xent.hip xent_fused: loss and dlogits = (softmax - onehot) / n_valid written in forward,
+# grad_out applied in backward).  MINGPT_XENT_FUSED=0 keeps the two-pass fwd / bwd kernels.
 _XENT_FUSED = os.environ.get("MINGPT_XENT_FUSED", "1") == "1"
-
-
-def _padded_weight(w, ld):
-    """[ld, D] copy of W with zero rows past V (cached per weight; refreshed every call)."""
-    wp = getattr(w, "_mg_padded", None)
-    if wp is None or wp.shape[0] != ld:
-        wp = torch.zeros(ld, w.shape[1], dtype=w.dtype, device=w.device)
-        w._mg_padded = wp
-    wp[: w.shape[0]].copy_(w)
-    return wp
 
 
 class HeadLossFn(_EngineFn):
@@ -246,12 +198,7 @@ class HeadLossFn(_EngineFn):
         V = w.shape[0]
         ld = (V + 127) // 128 * 128
         h, mean, rstd = C.layernorm_fwd(x, lnw, lnb, eps)
-        ctx.wpad = None
-        if _LMHEAD_BLAS and _big(h.shape[0], ld, h.shape[1]):
-            ctx.wpad = _padded_weight(w, ld)
-            logits = torch.mm(h, ctx.wpad.t())
-        else:
-            logits = G.gemm_nt(h, w, ld=ld)
+        logits = G.gemm_nt(h, w, ld=ld)
         fused = C.xent_fused(logits, targets, V) if _XENT_FUSED and any(ctx.needs_input_grad) else []
         if fused:  # the backward never reads the logits again
             out, dlogits = fused
@@ -281,10 +228,7 @@ class HeadLossFn(_EngineFn):
         del logits
         bw, mw = grad_target(w)
         G.gemm_tn_acc(dlogits, h, bw, n_valid=V)
-        if ctx.wpad is not None and _LMHEAD_DGRAD_BLAS:
-            dh = torch.mm(dlogits, ctx.wpad)  # zero rows past V meet the zero pad columns
-        else:
-            dh = G.gemm_dgrad(dlogits, w)  # W^T padded to the logits' row stride (zero columns)
+        dh = G.gemm_dgrad(dlogits, w)  # W^T padded to the logits' row stride (zero columns)
         blw, mlw = grad_target(lnw)
         blb, mlb = grad_target(lnb)
         dx = C.layernorm_bwd(dh, x, lnw, mean, rstd, blw, blb, None)

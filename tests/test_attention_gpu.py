@@ -9,12 +9,10 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.fixture(autouse=True, params=[1, 2, 3], ids=["bwd_persistent", "bwd_partials", "bwd4"])
+@pytest.fixture(autouse=True, params=[1, 2], ids=["bwd_persistent", "bwd_partials"])
 def bwd_mode(request):
-    """Every test under the backward schedules: one workgroup per (b, h) summing dQ in place, one
-    workgroup per (key block, b, h) with dQ partials + a finalize pass (8 waves x 32 keys), and the
-    one-wave-per-SIMD key-block kernel (4 waves x 64 keys; hd = 64 and T a multiple of 256 > 256,
-    else the 8-wave key-block kernel)."""
+    """Every test under both backward schedules: one workgroup per (b, h) summing dQ in place,
+    and one workgroup per (key block, b, h) with dQ partials + a finalize pass."""
     ext().attention_set_bwd_mode(request.param)
     yield request.param
     ext().attention_set_bwd_mode(0)
@@ -152,7 +150,7 @@ def _dense_keep(mask, B, T, H):
     kk = key % 64
     j = (key // 64) * 2 + ((kk >> 2) & 1)
     e = 16 * (kk >> 5) + 4 * ((kk >> 3) & 3) + (kk & 3)  # the forward lane's value index
-    bit = 8 * (e & 3) + (e >> 2)
+    bit = torch.where((e & 1) == 1, 31, 15) - (e >> 1)  # attn_common.h drop_bit: packed pair e >> 1
     w = words[:, j, :]  # [bh, key, q]
     return ((w >> bit[None, :, None]) & 1).transpose(1, 2).reshape(B, H, T, T).float()
 
@@ -171,7 +169,7 @@ def test_attention_fwd_head_dims(hd):
     att = att.masked_fill(~torch.ones(T, T, dtype=torch.bool, device=DEV).tril(), float("-inf"))
     for p in (0.0, 0.1):
         out, lse, mask = C.attention_fwd(qkv, B, T, H, p, 5)
-        keep = _dense_keep(mask, B, T, H) * (256.0 / (256 - round(p * 256))) if p > 0 else 1.0
+        keep = _dense_keep(mask, B, T, H) * (65536.0 / (65536 - round(p * 65536))) if p > 0 else 1.0
         ref = ((att.softmax(-1) * keep) @ v).transpose(1, 2).reshape(B * T, D)
         torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=3e-2)
         lse_ref = torch.logsumexp(att, -1) / torch.log(torch.tensor(2.0))
@@ -187,8 +185,8 @@ def test_attention_dropout_exact(T):
     D = H * hd
     qkv = torch.randn(B * T, 3 * D, device=DEV).to(torch.bfloat16)
     out, lse, mask = C.attention_fwd(qkv, B, T, H, p, 11)
-    thr = round(p * 256)
-    keep = _dense_keep(mask, B, T, H) * (256.0 / (256 - thr))
+    thr = round(p * 65536)
+    keep = _dense_keep(mask, B, T, H) * (65536.0 / (65536 - thr))
     qkv_r = qkv.float().requires_grad_()
     q, k, v = _split(qkv_r, B, T, H)
     att = (q @ k.transpose(-1, -2)) / hd ** 0.5
@@ -203,17 +201,20 @@ def test_attention_dropout_exact(T):
     torch.testing.assert_close(dqkv.float(), g, atol=3e-2 * max(1.0, scale / 4), rtol=5e-2)
 
 
-@pytest.mark.parametrize("p", [0.1, 0.6])  # thr <= 128 and > 128: both SWAR keep tests
+@pytest.mark.parametrize("p", [0.1, 0.6])  # thr <= 0x8000 and > 0x8000: both SWAR keep tests
 def test_attention_dropout_keep_rate(p):
-    """The forward's counter-hash dropout keeps ~(1 - thr/256) of the causal entries, uniformly."""
+    """The forward's counter-hash dropout keeps 1 - p of the causal entries (16-bit decisions: p is
+    exact to 1/65536), uniformly over heads; >= 1e7 draws at the bench shape's head dim."""
     C = ext()
-    B, T, H, hd = 2, 512, 4, 64
+    B, T, H, hd = 4, 1024, 8, 64
     qkv = torch.randn(B * T, 3 * H * hd, device=DEV).to(torch.bfloat16)
     _, _, mask = C.attention_fwd(qkv, B, T, H, p, 5)
     keep = _dense_keep(mask, B, T, H)
     causal = torch.ones(T, T, dtype=torch.bool, device=DEV).tril()
-    rate = keep[..., causal].mean().item()
-    assert abs(rate - (1 - round(p * 256) / 256)) < 0.005
+    kc = keep[..., causal]
+    assert kc.numel() >= 10_000_000
+    rate = kc.mean().item()
+    assert abs(rate - (1 - p)) < 0.001, rate
     # no structure across heads / rows: per-head rates agree
     per_head = keep[..., causal].mean(-1).flatten()
     assert (per_head - rate).abs().max().item() < 0.01

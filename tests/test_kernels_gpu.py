@@ -53,7 +53,7 @@ def test_embedding(p):
     wte, wpe = _bf(V, D, seed=5), _bf(T * 2, D, seed=6)
     out = C.embedding_fwd(idx, wte, wpe, p, 1234)
     ref = wte.float()[idx] + wpe.float()[:T].unsqueeze(0)
-    scale = 256.0 / (256 - round(256 * p))  # the 8-bit quantised keep scale (common.h rowdrop)
+    scale = 65536.0 / (65536 - round(65536 * p))  # the 16-bit keep scale (common.h rowdrop)
     if p == 0.0:
         _close(out, ref, atol=2e-2)
     else:
