@@ -275,3 +275,37 @@ def test_comm_exit_handler_does_not_pin_communicator():
     assert ref() is None
     _close_if_alive(ref)
     assert closed == [1]
+
+
+def _worker_subgroup_bcast(rank, world, port, out_dir):
+    _init(rank, world, port)
+    import torch.distributed as dist
+
+    from mingpt_distributed_amd.optim import FlatParamStore
+    from mingpt_distributed_amd.parallel.ddp import DataParallelEngine
+
+    sub = dist.new_group([1, 3])  # every rank creates it; only 1 and 3 use it
+    if rank in (1, 3):
+        torch.manual_seed(100 + rank)  # different weights per rank before the broadcast
+        m = torch.nn.Linear(4, 4)
+        store = FlatParamStore(m, device=torch.device("cpu"), bucket_numel=1 << 20)
+        eng = DataParallelEngine(store, process_group=sub, broadcast=False)
+        eng.broadcast_params(src=0)  # GROUP rank 0 = global rank 1
+        torch.save(store.master.clone(), os.path.join(out_dir, f"m{rank}.pt"))
+        eng.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_broadcast_params_src_is_a_group_rank(tmp_path):
+    """DataParallelEngine.broadcast_params reads ``src`` as a rank of the engine's process group on
+    both communicator paths (c10d converts it to the global rank): on the sub-group [1, 3], src 0
+    is global rank 1, whose weights both members end with."""
+    mp.spawn(_worker_subgroup_bcast, args=(4, _port(), str(tmp_path)), nprocs=4, join=True)
+    m1 = torch.load(tmp_path / "m1.pt", weights_only=True)
+    m3 = torch.load(tmp_path / "m3.pt", weights_only=True)
+    torch.manual_seed(101)
+    ref = torch.nn.Linear(4, 4)
+    assert torch.equal(m1, m3)
+    want = torch.cat([ref.weight.detach().reshape(-1), ref.bias.detach()]).sort().values
+    assert torch.equal(m1[: want.numel()].sort().values, want) or torch.equal(m1[m1 != 0].sort().values, want)
