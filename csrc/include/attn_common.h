@@ -46,8 +46,8 @@ inline int nks_for(int hd) {
 MG_DEVICE float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }  // v_exp_f32, no denorm fixup
 
 // Bit of score e (= 16 sub + r of a forward lane's 32 scores in a 64-key tile) in its dropout row
-// word: the packed pair j = e >> 1 (P operand word j) at bits 15 - j (low) and 31 - j (high).
-constexpr MG_DEVICE int drop_bit(int e) { return ((e & 1) ? 31 : 15) - (e >> 1); }
+// word: the packed pair j = e >> 1 (P operand word j) at bits j (low) and 16 + j (high).
+constexpr MG_DEVICE int drop_bit(int e) { return ((e & 1) << 4) + (e >> 1); }
 
 // 32-bit avalanche mixer (xorshift-multiply, "lowbias32" constants): a bijection with good
 // avalanche; the attention-dropout bytes are mix32 of distinct counters.

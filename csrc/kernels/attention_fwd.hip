@@ -31,6 +31,8 @@
 //  * P is converted to bf16 in registers and used directly as the B operand of O^T = V^T P^T;
 //    V^T fragments come from LDS with ds_read_b64_tr_b16 in the matching permuted key order.
 //  * heaviest (last) query blocks are launched first; fully-masked K tiles are skipped per wave.
+#include <type_traits>
+
 #include "attn_common.h"
 #include "kernels.h"
 
@@ -47,8 +49,8 @@ namespace {
 // Keep bits (keep iff a 16-bit uniform >= thr) as "row words": word (bh, j, q), j = 2 * tile + h, covers
 // the 32 scores one forward lane holds for query q in 64-key tile `tile`, half h: value
 // e = 16 * sub + r  <->  key 64 * tile + 32 * sub + 4 * h + (r & 3) + 8 * (r >> 2), at bit
-// drop_bit(e) = (e & 1 ? 31 : 15) - (e >> 1) (attn_common.h): the two scores of packed pair
-// j = e >> 1 (one bf16x2 word of the P operand) sit at bits 15 - j and 31 - j, so one shift and one
+// drop_bit(e) = 16 (e & 1) + (e >> 1) (attn_common.h): the two scores of packed pair
+// j = e >> 1 (one bf16x2 word of the P operand) sit at bits j and 16 + j, so one shift and one
 // packed 16-bit arithmetic shift make the pair's 32-bit keep mask (attn_fwd_pipe_kernel).  Stored
 // [bh][j][q]: lanes of consecutive queries read consecutive words in both passes; the backward
 // tests a per-lane bit.  Randomness: one lowbias32 mix of the word index and seed, then xorshift32
@@ -70,8 +72,9 @@ __global__ __launch_bounds__(256) void attn_dropmask_kernel(uint32_t* __restrict
   const int q = 32 * G + (lane & 31), h = lane >> 5;
   const uint64_t sd = eff_seed(seed, sofs);
   const uint32_t key = (uint32_t)sd ^ mix32((uint32_t)(sd >> 32) + 0x9E3779B9u);
-  // exact 16-bit decisions (keep iff a 16-bit uniform >= thr, thr = round(65536 p) <= 65535)
-  const uint32_t kadd = (thr <= 0x8000u ? 0x8000u - thr : 0x10000u - thr) * 0x00010001u;
+  // exact 16-bit decisions (keep iff a 16-bit uniform u >= thr, thr = round(65536 p) in [1, 65535]):
+  // both halves at once, min(sat(u - (thr - 1)), 1) = [u >= thr] (v_pk_sub_u16 clamp, v_pk_min_u16)
+  const uint32_t tm1 = (thr - 1u) * 0x00010001u, one = 0x00010001u;
   const int tmax = min(nt - 1, G >> 1);
   for (int t = 0; t <= tmax; ++t) {
     const int j = 2 * t + h;
@@ -84,11 +87,11 @@ __global__ __launch_bounds__(256) void attn_dropmask_kernel(uint32_t* __restrict
         x ^= x << 13;
         x ^= x >> 17;
         x ^= x << 5;
-        // SWAR over the two 16-bit halves: bit 15 of half k <- (half >= thr); shifted right by w
-        // the two decisions land at bits 15 - w, 31 - w (values e = 2w, 2w + 1): drop_bit(e)
-        const uint32_t y = (x & 0x7fff7fffu) + kadd;
-        const uint32_t k15 = (thr <= 0x8000u ? (y | x) : (y & x)) & 0x80008000u;
-        bits |= k15 >> w;
+        // the two decisions land at bits w, 16 + w (values e = 2w, 2w + 1): drop_bit(e)
+        // (asm: the builtins became two compares and selects per half)
+        uint32_t k;
+        asm("v_pk_sub_u16 %0, %1, %2 clamp\n\tv_pk_min_u16 %0, %0, %3" : "=&v"(k) : "v"(x), "v"(tm1), "v"(one));
+        bits |= k << w;
       }
       dmask[((long)bh * ntw + j) * T + q] = bits;
     }
@@ -389,10 +392,10 @@ MG_DEVICE float max3f(float a, float b, float c) {
   return r;
 }
 
-// keep mask of packed pair j (bf16x2 word j of a lane's P operand): bits 15 - j and 31 - j of the
+// keep mask of packed pair j (bf16x2 word j of a lane's P operand): bits j and 16 + j of the
 // row word, each sign-extended over its 16-bit half (one shift + one v_pk_ashrrev_i16)
 MG_DEVICE uint32_t pair_mask(uint32_t kw, int j) {
-  const s16x2 mk = __builtin_bit_cast(s16x2, kw << j) >> (s16x2){15, 15};
+  const s16x2 mk = __builtin_bit_cast(s16x2, kw << (15 - j)) >> (s16x2){15, 15};
   return __builtin_bit_cast(uint32_t, mk);
 }
 
@@ -413,7 +416,7 @@ MG_DEVICE uint32_t pair_mask(uint32_t kw, int j) {
 //    a block; then o, l and the already-issued next tile are rescaled in place (no recompute).
 //  * the row sum l = sum of the undropped bf16 P is an MFMA against a ones operand (4 per tile)
 //    instead of 32 VALU adds per lane: the matrix pipe has the slack, the vector pipe does not.
-//  * dropout on the packed bf16 P: pair j's keep bits sit at 15 - j and 31 - j of the lane's row
+//  * dropout on the packed bf16 P: pair j's keep bits sit at j and 16 + j of the lane's row
 //    word (drop_bit), so its 32-bit mask is one shift + one v_pk_ashrrev_i16 and the drop one AND
 //    per pair (1.5 VALU per score; was a bit-field extract + AND per fp32 score).
 //  * the causal mask touches only each wave's last (diagonal) tile.
@@ -546,8 +549,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
     // causal mask of a wave's diagonal tile t: key 64 t + k0 + 4 h32 + (r & 3) + 8 (r >> 2) > query
     // -> -inf (p = 0).  Applied to S(t) once, right after its MFMAs were issued.
     auto mask_diag = [&](f32x16& c0, f32x16& c1, int t) __attribute__((always_inline)) {
-      int lim = myq - 64 * t - 4 * h32;
-      asm volatile("" : "+v"(lim));
+      const int lim = myq - 64 * t - 4 * h32;
       auto mask = [&](f32x16& c, int k0) __attribute__((always_inline)) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) c[r] = (k0 + (r & 3) + 8 * (r >> 2) > lim) ? -__builtin_huge_valf() : c[r];
@@ -566,7 +568,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
       }
       return __builtin_bit_cast(bf16x8, make_uint4(u[0], u[1], u[2], u[3]));
     };
-    // dropped P: pair j's mask = sign-extended bits 15 - j / 31 - j of the row word
+    // dropped P: pair j's mask = sign-extended bits j / 16 + j of the row word
     auto dropped = [&](const bf16x8& pu, int j, uint32_t kw) __attribute__((always_inline)) -> bf16x8 {
       if constexpr (!DROP) return pu;
       const uint4 u = __builtin_bit_cast(uint4, pu);
@@ -577,10 +579,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
     // One tile of one wave: S(t+1) issued first (speculative on the diagonal tile), then S(t)'s
     // range check, exp2, packing and dropout (VALU beside those MFMAs), the rare rescale, then
     // O^T += V^T (Z P)^T and l^T += 1^T P^T.
-    auto compute = [&](f32x16& c0, f32x16& c1, f32x16& n0, f32x16& n1, int t, uint32_t kw) __attribute__((always_inline)) {
+    // DIAG: the wave's last (diagonal) tile t == tw: S(t) masked in place first, no S(t+1)
+    auto compute = [&](f32x16& c0, f32x16& c1, f32x16& n0, f32x16& n1, int t, uint32_t kw, auto diag_tag) __attribute__((always_inline)) {
+      constexpr bool DIAG = decltype(diag_tag)::value;
       const int u = u0 + t;
       const char* sv = sV + (u & 1) * TILE;
-      scores(n0, n1, sK + ((u + 1) & 1) * TILE);
+      if constexpr (DIAG) mask_diag(c0, c1, t);
+      else scores(n0, n1, sK + ((u + 1) & 1) * TILE);
       float mx = max3f(c0[0], c0[1], c0[2]);
 #pragma unroll
       for (int r = 3; r < 15; r += 2) mx = max3f(mx, c0[r], c0[r + 1]);
@@ -607,8 +612,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
         negm = -m;
         c0 -= d;
         c1 -= d;
-        n0 -= d;  // S(t+1) was issued against the old m
-        n1 -= d;
+        if constexpr (!DIAG) {
+          n0 -= d;  // S(t+1) was issued against the old m
+          n1 -= d;
+        }
         rs = 0.f;
         pu00 = expack(c0, 0, rs), pu01 = expack(c0, 1, rs), pu10 = expack(c1, 0, rs), pu11 = expack(c1, 1, rs);
       }
@@ -626,38 +633,52 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
       pv(pd01, pu01, 16 * ROWB);
       pv(pd10, pu10, 32 * ROWB);
       pv(pd11, pu11, 48 * ROWB);
-      if (t + 1 == tw) mask_diag(n0, n1, t + 1);
     };
 
     // block prologue: S(0) from K(u0) (staged), then a barrier before anyone restages that slot
-    uint32_t kw_cur = (DROP && tw >= 0) ? row_word(0) : 0u;
+    uint32_t kw_cur = DROP ? row_word(0) : 0u;
     f32x16 sA0, sA1, sB0, sB1;
-    if (tw >= 0) {
-      scores(sA0, sA1, sK + (u0 & 1) * TILE);
-      if (tw == 0) mask_diag(sA0, sA1, 0);
-    }
+    if (tw >= 0) scores(sA0, sA1, sK + (u0 & 1) * TILE);
     __syncthreads();
 
-    // iteration t (stream u = u0 + t): S(t+1) -> n, softmax / PV of tile t from c, stage K(u+2),
-    // V(u+1) into the slots K(u) / V(u-1) held (read before the previous barrier)
+    // iteration t (stream u = u0 + t): softmax / PV of tile t from c (and S(t+1) -> n unless it
+    // is the wave's diagonal tile), stage K(u+2), V(u+1) into the slots K(u) / V(u-1) held (read
+    // before the previous barrier).  Every load and store is unconditional (indices clamped; a
+    // stream tile past the end lands in a slot nobody reads again): conditional loads made hipcc
+    // wait vmcnt(0) ahead of the next iteration's loads -- a full memory latency per tile.
     const int nt = bi ? ntB : ntA;
-    auto iteration = [&](int t, f32x16& c0, f32x16& c1, f32x16& n0, f32x16& n1) __attribute__((always_inline)) {
+    auto stage = [&](int t, auto&& body) __attribute__((always_inline)) {
       const int u = u0 + t;
       uint4 rk[2], rv[2];
-      const bool sk2 = u + 2 < nall, sv1 = u + 1 < nall;
-      if (sk2) load_k(rk, u + 2);
-      if (sv1) load_v(rv, u + 1);
-      const uint32_t kw_next = (DROP && t + 1 <= tw) ? row_word(t + 1) : 0u;
-      if (t <= tw) compute(c0, c1, n0, n1, t, kw_cur);
+      load_k(rk, min(u + 2, nall - 1));
+      load_v(rv, min(u + 1, nall - 1));
+      const uint32_t kw_next = DROP ? row_word(min(t + 1, max(tw, 0))) : 0u;
+      body();
       kw_cur = kw_next;
-      if (sk2) store_tile(sK + (u & 1) * TILE, rk);
-      if (sv1) store_tile(sV + ((u + 1) & 1) * TILE, rv);
+      store_tile(sK + (u & 1) * TILE, rk);
+      store_tile(sV + ((u + 1) & 1) * TILE, rv);
       __syncthreads();
     };
-    for (int t = 0; t < nt; t += 2) {
-      iteration(t, sA0, sA1, sB0, sB1);
-      if (t + 1 < nt) iteration(t + 1, sB0, sB1, sA0, sA1);
+    // Per wave: steady tiles t < tw, the diagonal tile tw, then idle tiles up to the workgroup's
+    // nt.  The trip counts differ between waves but every iteration has exactly one barrier, so
+    // waves 0-1 at their diagonal meet waves 2-3 at their last steady tile.  No iteration body
+    // holds both compute variants (a steady / diagonal branch inside one body spilled).
+    int t = 0;
+    if (tw >= 0) {
+      for (; t + 1 < tw; t += 2) {
+        stage(t, [&]() __attribute__((always_inline)) { compute(sA0, sA1, sB0, sB1, t, kw_cur, std::false_type{}); });
+        stage(t + 1, [&]() __attribute__((always_inline)) { compute(sB0, sB1, sA0, sA1, t + 1, kw_cur, std::false_type{}); });
+      }
+      if (t < tw) {  // odd count: one more steady tile; S(tw) then sits in the B set
+        stage(t, [&]() __attribute__((always_inline)) { compute(sA0, sA1, sB0, sB1, t, kw_cur, std::false_type{}); });
+        ++t;
+        sA0 = sB0;
+        sA1 = sB1;
+      }
+      stage(t, [&]() __attribute__((always_inline)) { compute(sA0, sA1, sB0, sB1, t, kw_cur, std::true_type{}); });
+      ++t;
     }
+    for (; t < nt; ++t) stage(t, []() {});
 
     // block epilogue: O = o * dscale / l, lse = m + log2 l (log2 domain)
     if (myq < a.T) {

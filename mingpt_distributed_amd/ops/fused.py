@@ -23,6 +23,7 @@ import os
 import torch
 
 from . import gemm as G
+from . import streams
 from ._ext import ext
 from .grads import before_use, finish, grad_target, note_use
 
@@ -59,9 +60,15 @@ def _dgrad(dy, w):
     return G.gemm_dgrad(dy, w)
 
 
-def _wgrad(dy, x, main_grad):
-    """main_grad += dY^T @ X (gemm.hip split-K, fp32 accumulate in the epilogue)."""
-    G.gemm_tn_acc(dy, x, main_grad)
+def _wgrad(dy, x, target):
+    """main_grad += dY^T @ X (gemm.hip split-K, fp32 accumulate in the epilogue).  ``target`` is
+    grad_target()'s (buffer, is_main): a main_grad accumulation runs on the weight-gradient
+    stream (streams.py), beside the data gradients; a gradient returned to autograd in order."""
+    buf, is_main = target
+    if is_main:
+        streams.run_wgrad(lambda: G.gemm_tn_acc(dy, x, buf), dy, x)
+    else:
+        G.gemm_tn_acc(dy, x, buf)
 
 
 class _EngineFn(torch.autograd.Function):
@@ -141,13 +148,13 @@ class TransformerBlockFn(_EngineFn):
         else:
             dz = dx2
             C.bias_grad(dz, g[id(bp)][0])
-        _wgrad(dz, u, g[id(wp)][0])
+        _wgrad(dz, u, g[id(wp)])
         if _FC_DBIAS_FUSED:  # fc bias gradient: column sums of dpre in the GELU' epilogue
             dpre = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=gd, dbias=g[id(bfc)][0])
         else:
             dpre = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=gd)
             C.bias_grad(dpre, g[id(bfc)][0])
-        _wgrad(dpre, h2, g[id(wfc)][0])
+        _wgrad(dpre, h2, g[id(wfc)])
         dh2 = _dgrad(dpre, wfc)
         dx1 = C.layernorm_bwd(dh2, x1, ln2w, mean2, rstd2, g[id(ln2w)][0], g[id(ln2b)][0], dx2)
         # ---- attention: x1 = x + drop(attn(h Wqkv^T + bqkv) Wo^T + bo)
@@ -156,7 +163,7 @@ class TransformerBlockFn(_EngineFn):
         else:
             dz = dx1
             C.bias_grad(dz, g[id(bo)][0])
-        _wgrad(dz, y, g[id(wo)][0])
+        _wgrad(dz, y, g[id(wo)])
         hd = wo.shape[0] // H
         delta = None
         if _DELTA_FUSED and hd in (8, 16, 32, 64):
@@ -172,7 +179,7 @@ class TransformerBlockFn(_EngineFn):
             dqkv = C.attention_bwd(qkv, y, dy, lse, amask, B, T, H, float(p_attn), ctx.seeds[0],
                                    None, delta)
             C.bias_grad(dqkv, g[id(bqkv)][0])
-        _wgrad(dqkv, h, g[id(wqkv)][0])
+        _wgrad(dqkv, h, g[id(wqkv)])
         dh = _dgrad(dqkv, wqkv)
         dx = C.layernorm_bwd(dh, x, ln1w, mean1, rstd1, g[id(ln1w)][0], g[id(ln1b)][0], dx1)
         outs = [finish(prm, *g[id(prm)]) for prm in ctx.params]

@@ -238,6 +238,9 @@ class FusedAdamW:
         return self.norm_buf[1]
 
     def step(self, grad_scale: float = 1.0, lr: Optional[float] = None):
+        from .ops import streams
+
+        streams.join()  # weight gradients still on the side stream (ops/streams.py)
         s = self.store
         lr = self.param_groups[0]["lr"] if lr is None else lr
         self.step_count += 1

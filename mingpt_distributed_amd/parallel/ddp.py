@@ -45,6 +45,7 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from ..ops import streams
 from ..optim import FlatParamStore
 
 
@@ -193,7 +194,9 @@ class DataParallelEngine:
     def _launch(self, b: _Bucket):
         if self.next_launch == 0:
             self.inflight = []
-        b.work = self._issue(b)
+        # after the bucket's weight gradients, which may still run on the side stream
+        with streams.collective_stream(self.store.device):
+            b.work = self._issue(b)
         self.inflight.append((self.next_launch, b.end - b.start, b.work))
 
     def _issue(self, b: _Bucket, wire: Optional[torch.Tensor] = None):
@@ -266,6 +269,7 @@ class DataParallelEngine:
 
     def finish(self):
         """Launch what is left (parameters unused this step), wait, and reset for the next step."""
+        streams.join()
         if not self.active:
             return
         if self.sync_enabled:

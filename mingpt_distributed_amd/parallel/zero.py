@@ -40,6 +40,7 @@ from typing import List, Optional, Set
 import torch
 import torch.distributed as dist
 
+from ..ops import streams
 from ..optim import FlatParamStore, FusedAdamW, make_chunk_table
 from .ddp import DataParallelEngine, _Bucket
 
@@ -221,6 +222,7 @@ class ZeroAdamW(FusedAdamW):
                 dist.all_reduce(self.norm_buf[:1], group=self.engine.pg)
 
     def step(self, grad_scale: float = 1.0, lr: Optional[float] = None):
+        streams.join()  # weight gradients still on the side stream (ops/streams.py)
         s, e = self.store, self.engine
         lr = self.param_groups[0]["lr"] if lr is None else lr
         self.step_count += 1

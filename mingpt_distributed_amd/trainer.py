@@ -32,6 +32,7 @@ from typing import Any, Dict, List, Optional
 import torch
 from torch.utils.data import DataLoader, Dataset
 
+from .ops import streams
 from .optim import FlatParamStore, FusedAdamW, param_groups
 from .parallel import dist as D
 from .parallel.ddp import DataParallelEngine
@@ -183,6 +184,7 @@ class StepEngine:
                 _, loss = self.model(x, y)
             with self._range("mingpt::backward"):
                 (loss * scale if scale != 1.0 else loss).backward()
+                streams.join()  # the block weight gradients ran on the side stream
             if self.dp is not None:
                 ev = None
                 if self.measure_comm and sync and self.device.type == "cuda":
