@@ -494,16 +494,20 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
   const int ta1 = tr_off(4 * h32 + trq, 32 + trc), tb1 = tr_off(8 + 4 * h32 + trq, 32 + trc);
   const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u));
 
-  // ---- prologue staging: K(0), V(0), K(1) loads in flight together
+  // ---- prologue staging: K(0), V(0), K(1) loads in flight together, then K(2), V(1) into the
+  // staging registers (written at iteration 0's start)
+  uint4 rk[2], rv[2];
   {
-    uint4 rk[2], rv[2], rk1[2];
+    uint4 rk1[2];
     load_k(rk, 0);
     load_v(rv, 0);
-    if (nall > 1) load_k(rk1, 1);
+    load_k(rk1, min(1, nall - 1));
     store_tile(sK, rk);
     store_tile(sV, rv);
-    if (nall > 1) store_tile(sK + TILE, rk1);
+    store_tile(sK + TILE, rk1);
   }
+  load_k(rk, min(2, nall - 1));
+  load_v(rv, min(1, nall - 1));
   __syncthreads();
 
   for (int bi = 0; bi < nblk; ++bi) {
@@ -641,22 +645,23 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
     if (tw >= 0) scores(sA0, sA1, sK + (u0 & 1) * TILE);
     __syncthreads();
 
-    // iteration t (stream u = u0 + t): softmax / PV of tile t from c (and S(t+1) -> n unless it
-    // is the wave's diagonal tile), stage K(u+2), V(u+1) into the slots K(u) / V(u-1) held (read
-    // before the previous barrier).  Every load and store is unconditional (indices clamped; a
-    // stream tile past the end lands in a slot nobody reads again): conditional loads made hipcc
-    // wait vmcnt(0) ahead of the next iteration's loads -- a full memory latency per tile.
+    // iteration t (stream u = u0 + t): first write the staging registers -- K(u+2), V(u+1),
+    // loaded one iteration ago -- into the slots K(u) / V(u-1) held (read before the previous
+    // barrier) and re-issue them at once for K(u+3), V(u+2), so a load has a whole iteration and
+    // its barrier to land; then softmax / PV of tile t from c (and S(t+1) -> n unless it is the
+    // wave's diagonal tile).  Every load and store is unconditional (indices clamped; a stream
+    // tile past the end lands in a slot nobody reads again): conditional loads made hipcc wait
+    // vmcnt(0) ahead of the next iteration's loads -- a full memory latency per tile.
     const int nt = bi ? ntB : ntA;
     auto stage = [&](int t, auto&& body) __attribute__((always_inline)) {
       const int u = u0 + t;
-      uint4 rk[2], rv[2];
-      load_k(rk, min(u + 2, nall - 1));
-      load_v(rv, min(u + 1, nall - 1));
+      store_tile(sK + (u & 1) * TILE, rk);
+      store_tile(sV + ((u + 1) & 1) * TILE, rv);
+      load_k(rk, min(u + 3, nall - 1));
+      load_v(rv, min(u + 2, nall - 1));
       const uint32_t kw_next = DROP ? row_word(min(t + 1, max(tw, 0))) : 0u;
       body();
       kw_cur = kw_next;
-      store_tile(sK + (u & 1) * TILE, rk);
-      store_tile(sV + ((u + 1) & 1) * TILE, rv);
       __syncthreads();
     };
     // Per wave: steady tiles t < tw, the diagonal tile tw, then idle tiles up to the workgroup's

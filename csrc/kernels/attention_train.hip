@@ -283,37 +283,51 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
     const uint64_t q_total = (uint64_t)a.B * a.T * ld * 2, do_total = (uint64_t)a.B * a.T * a.D * 2;
     const uint64_t q_org = (uint64_t)((const char*)Qg - (const char*)a.qkv);
     const uint64_t do_org = (uint64_t)((const char*)dOg - (const char*)a.dout);
-    float rl = 0.f;
     constexpr int NMW = KW * BQ / NT;  // keep words staged per thread
     uint32_t rmw[NMW];
-#pragma unroll
-    for (int i = 0; i < NMW; ++i) rmw[i] = 0xffffffffu;  // no dropout: every key kept
+    // this (b, h)'s keep words [ntw][T] (attn_dropmask_kernel layout); an empty range without dropout
+    const __amdgpu_buffer_rsrc_t mw_rs =
+        kv_rsrc(reinterpret_cast<const bf16_t*>(a.thr ? a.dmask : nullptr) , a.thr ? (uint64_t)(bh + 1) * ntw * a.T * 4 : 0,
+                a.thr ? (uint64_t)bh * ntw * a.T * 4 : 0);
+    // Every load below is unconditional (indices clamped) and its raw value is only selected at
+    // commit(): a load whose result a select right behind it needed (hipcc sank it into a branch)
+    // made the wave wait vmcnt(0) just after this tile's Q / dO prefetch was issued -- a full
+    // memory latency per tile in every wave.
+    float rl_raw = 0.f;
+    const uint32_t nodrop = a.thr ? 0u : 0xffffffffu;  // no dropout: every key kept
     auto issue = [&](int qt) {
       stq::load_buf(rq, a.qkv, q_total, q_org + (uint64_t)qt * BQ * ld * 2, oq);
       stq::load_buf(rd, a.dout, do_total, do_org + (uint64_t)qt * BQ * a.D * 2, od);
       const int t = threadIdx.x;
-      if (t < 2 * BQ) {
-        const int q = qt * BQ + (t & (BQ - 1));
-        rl = q < a.T ? (t < BQ ? -lseg[q] : dlg[q] * ddl) : 0.f;  // -lse: the S init (K holds c K)
-      }
-      if (a.thr) {  // word j of query row q -> sMW[j * BQ + q]
+      // threads [0, BQ): lse, [BQ, 2 BQ): delta (the rest load a valid row and drop it)
+      rl_raw = ((t & BQ) ? dlg : lseg)[min(qt * BQ + (t & (BQ - 1)), a.T - 1)];
+      // keep words: word j of query row q -> sMW[j * BQ + q] (an empty descriptor without dropout)
 #pragma unroll
-        for (int i = 0; i < NMW; ++i) {
-          const int u = t + NT * i;
-          const int q = qt * BQ + (u & (BQ - 1)), j = u / BQ;
-          rmw[i] = (q < a.T && t0w + j < ntw) ? a.dmask[((long)bh * ntw + t0w + j) * a.T + q] : 0u;
-        }
+      for (int i = 0; i < NMW; ++i) {
+        const int u = t + NT * i;
+        const int q = qt * BQ + (u & (BQ - 1)), j = u / BQ;
+        const uint32_t off = (uint32_t)(((t0w + min(j, ntw - 1 - t0w)) * a.T + min(q, a.T - 1)) * 4);
+        rmw[i] = __builtin_amdgcn_raw_buffer_load_b32(mw_rs, off, 0, 0);
       }
     };
-    auto commit = [&]() {
+    auto commit = [&](int qt) {
       stq::store(smem + OFF_Q, rq);
       stq::store(smem + OFF_DO, rd);
-      if (threadIdx.x < 2 * BQ) reinterpret_cast<float*>(smem + OFF_L)[threadIdx.x] = rl;
+      const int t = threadIdx.x;
+      const int ql = qt * BQ + (t & (BQ - 1));
+      // -lse: the S init (K holds c K); delta' = delta / dscale (bwd_softmax_grad)
+      const float rl = ql < a.T ? ((t & BQ) ? rl_raw * ddl : -rl_raw) : 0.f;
+      if (t < 2 * BQ) reinterpret_cast<float*>(smem + OFF_L)[t] = rl;
 #pragma unroll
-      for (int i = 0; i < NMW; ++i) reinterpret_cast<uint32_t*>(smem + OFF_MW)[threadIdx.x + NT * i] = rmw[i];
+      for (int i = 0; i < NMW; ++i) {
+        const int u = t + NT * i;
+        const int q = qt * BQ + (u & (BQ - 1)), j = u / BQ;
+        const uint32_t w = ((q < a.T && t0w + j < ntw) ? rmw[i] : 0u) | nodrop;
+        reinterpret_cast<uint32_t*>(smem + OFF_MW)[u] = w;
+      }
     };
     issue(qt0);
-    commit();
+    commit(qt0);
     __syncthreads();
 
     for (int qt = qt0; qt < nqt; ++qt) {
@@ -489,7 +503,7 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
           }
         }
       }
-      if (more) commit();
+      if (more) commit(qt + 1);
       __syncthreads();
     }
 

@@ -10,9 +10,14 @@ tiles with the other's blocks (gpt2-xl's 175-tile weight gradients leave 81 of 2
 own; the ~30 us elementwise kernels leave the matrix cores idle).
 
 Ordering contract:
-* :func:`run_wgrad` -- the side stream waits for everything the compute stream has issued so far,
-  runs the GEMM, and the inputs are ``record_stream``'d so the caching allocator does not hand
-  their memory out before the side stream is done with it.
+* :func:`run_wgrad` -- the side stream waits for everything the compute stream has issued so far
+  and runs the GEMM.  The inputs' lifetime is bounded by a LAGGED join instead of
+  ``record_stream``: the compute stream waits for weight gradient k - LAG (an event, usually long
+  complete) before weight gradient k is issued, and only then are that one's inputs released, so
+  the caching allocator can hand their memory to later compute-stream work at once.
+  (``record_stream`` made every freed activation unusable until the CPU -- which runs a whole
+  backward ahead of the GPU -- saw its event complete: at B = 128 the allocator grew instead of
+  reusing, 600-720 ms per step against 127.)
 * :func:`join` -- the compute stream waits for every weight gradient issued so far.  Called after
   ``loss.backward()`` (``StepEngine.forward_backward``) and by every reader of ``main_grad``
   (the data-parallel engines' ``finish``, the optimizer step).
@@ -21,20 +26,30 @@ Ordering contract:
   its bucket without making the compute stream wait.
 
 Only parameters that own a ``main_grad`` use the stream (their buffer is read after a join); a
-gradient that autograd returns is computed in order.  ``MINGPT_WGRAD_STREAM=0`` runs everything
-on the compute stream.  Replaces nothing in the reference: its DDP backward is one stream
+gradient that autograd returns is computed in order.  ``MINGPT_WGRAD_STREAM``: ``auto`` (default;
+small weight gradients only, see ``_MODE``), ``1`` always, ``0`` never.  Replaces nothing in the reference: its DDP backward is one stream
 (``/root/reference/mingpt/trainer.py:71``).
 """
 from __future__ import annotations
 
 import contextlib
 import os
-from typing import Callable, Dict
+from collections import deque
+from typing import Callable, Deque, Dict, Tuple
 
 import torch
 
-_ENABLED = os.environ.get("MINGPT_WGRAD_STREAM", "1") == "1"
+# "auto" (default): the side stream for weight gradients over at most _AUTO_TOKENS rows (tokens),
+# where their tiles underfill the GPU -- measured on one box (profiles/round4_wgrad_stream_ab.txt):
+# gpt2-xl at 16k tokens +1.2 %, GPT-2 at 131k tokens -1.1 % (its weight gradients already fill
+# the chip; the concurrency only adds contention).  "1" always, "0" never.
+_MODE = os.environ.get("MINGPT_WGRAD_STREAM", "auto").lower()
+_ENABLED = _MODE != "0"
+_AUTO_TOKENS = int(os.environ.get("MINGPT_WGRAD_STREAM_TOKENS", "32768"))
+# weight gradients in flight before the compute stream waits for the oldest (4 = one block)
+_LAG = max(1, int(os.environ.get("MINGPT_WGRAD_LAG", "4")))
 _side: Dict[int, "torch.cuda.Stream"] = {}
+_inflight: Dict[int, Deque[Tuple["torch.cuda.Event", tuple]]] = {}
 _pending: set = set()
 
 
@@ -42,11 +57,18 @@ def enabled() -> bool:
     return _ENABLED
 
 
-def set_enabled(on: bool) -> None:
-    """Switch the side stream on / off (tests, A/B).  Joins first so nothing is left in flight."""
-    global _ENABLED
+def set_enabled(on: bool, mode: str = "1") -> None:
+    """Switch the side stream on (``mode`` "1": every weight gradient, "auto": small ones) or off
+    (tests, A/B).  Joins first so nothing is left in flight."""
+    global _ENABLED, _MODE
     join()
     _ENABLED = bool(on)
+    _MODE = mode if on else "0"
+
+
+def use_for(tokens: int) -> bool:
+    """Whether a weight gradient over ``tokens`` rows goes to the side stream."""
+    return _ENABLED and (_MODE != "auto" or tokens <= _AUTO_TOKENS)
 
 
 def _stream(dev: torch.device) -> "torch.cuda.Stream":
@@ -59,16 +81,22 @@ def _stream(dev: torch.device) -> "torch.cuda.Stream":
 
 def run_wgrad(fn: Callable[[], None], *inputs: torch.Tensor) -> None:
     """Run ``fn`` (a weight-gradient accumulation reading ``inputs``) on the side stream."""
-    if not _ENABLED or not inputs[0].is_cuda:
+    if not inputs[0].is_cuda or not use_for(inputs[0].shape[0]):
         fn()
         return
     dev = inputs[0].device
     s = _stream(dev)
-    s.wait_stream(torch.cuda.current_stream(dev))
+    cur = torch.cuda.current_stream(dev)
+    q = _inflight.setdefault(s.device.index, deque())
+    while len(q) >= _LAG:  # the oldest weight gradient's inputs may now be reused by `cur`
+        ev, _ = q.popleft()
+        cur.wait_event(ev)
+    s.wait_stream(cur)
     with torch.cuda.stream(s):
         fn()
-    for t in inputs:
-        t.record_stream(s)
+    ev = torch.cuda.Event()
+    ev.record(s)
+    q.append((ev, inputs))
     _pending.add(s.device.index)
 
 
@@ -78,6 +106,7 @@ def join() -> None:
         return
     for idx in list(_pending):
         torch.cuda.current_stream(idx).wait_stream(_side[idx])
+        _inflight.get(idx, deque()).clear()  # inputs released only after the wait
     _pending.clear()
 
 

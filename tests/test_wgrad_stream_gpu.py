@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _grads(base, x, y, on):
-    streams.set_enabled(on)
+    streams.set_enabled(on, "1")  # every weight gradient on the side stream, whatever its size
     try:
         eng = StepEngine(copy.deepcopy(base), lr=1e-3)
         eng.forward_backward(x, y)
@@ -23,7 +23,7 @@ def _grads(base, x, y, on):
         torch.cuda.synchronize()
         return eng.store.grad.clone()
     finally:
-        streams.set_enabled(True)
+        streams.set_enabled(True, "auto")
 
 
 @pytest.mark.parametrize("n_embed,n_head", [(256, 4), (768, 12)])
@@ -41,11 +41,20 @@ def test_side_stream_grads_match_in_order(n_embed, n_head):
 
 
 def test_side_stream_training_steps_reduce_loss():
+    streams.set_enabled(True, "1")
     torch.manual_seed(0)
     cfg = GPTConfig(n_layer=2, n_head=4, n_embed=256, vocab_size=1000, block_size=128,
                     embed_drop=0.1, resid_drop=0.1, attn_drop=0.1)
     eng = StepEngine(GPT(cfg, verbose=False), lr=1e-3)
     x = torch.randint(0, 1000, (8, 128), device="cuda")
     y = torch.roll(x, -1, 1)
-    losses = [eng.train_step([(x, y)]).item() for _ in range(20)]
+    try:
+        losses = [eng.train_step([(x, y)]).item() for _ in range(20)]
+    finally:
+        streams.set_enabled(True, "auto")
     assert losses[-1] < losses[0] - 1.0, losses
+
+
+def test_auto_mode_picks_small_weight_gradients():
+    streams.set_enabled(True, "auto")
+    assert streams.use_for(16384) and not streams.use_for(131072)
