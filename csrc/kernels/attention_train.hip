@@ -185,6 +185,9 @@ MG_DEVICE void tr_reduce32(float (&v)[NV], int lane) {
 //  * attention dropout: the forward's keep bits (attn_dropmask_kernel), one word per query and
 //    32-key half tile, staged BQ queries x KW words per tile.
 //  * BQ = 128 queries per tile (key-block mode, hd <= 64): the dS^T image is two 64-query halves.
+// Timing-only ablation builds (MG_EXTRA_FLAGS=-DMG_ABL_BWD_<X>, outputs wrong on purpose; PERF.md
+// round 4): NOSM (no softmax-gradient VALU), NOKV (no dV / dK MFMAs), NOSTAGE (no next-tile
+// loads), NODQST (no dQ stores).
 template <int NKS, int KW, bool PERSIST>
 __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) {
   constexpr int BQ = bwd_bq<NKS, PERSIST>();
@@ -342,7 +345,9 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
       // one to reach the tile writes bf16
       const int last_kb = min(nkb - 1, (qbase + BQ - 1) / KB);
       const bool first = part || kb == 0, last = !part && kb == last_kb;
+#ifndef MG_ABL_BWD_NOSTAGE
       if (more) issue(qt + 1);
+#endif
       // previous key blocks' dQ sums of this wave's tiles: LDS-DMA'd now (no registers held),
       // added after the dQ MFMAs (a load in the store loop exposed a memory latency per tile)
       float* pvs = reinterpret_cast<float*>(smem + OFF_PV) + (my_split == 0 ? w : 0) * NTW * 16 * 64;
@@ -407,15 +412,25 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
                                                        0, 0, 0);
         }
         // wave-uniform: only diagonal / past-T tiles pay for the causal mask
+#ifdef MG_ABL_BWD_NOSM
+        if (false)
+#else
         if (wave_kmin + 31 > qsub0 || qsub0 + 31 >= a.T)
+#endif
           bwd_softmax_grad<true>(sacc, dp, dl, mwr, a.T, mykey, mw_bit, qsub0 + 4 * h32);
+#ifndef MG_ABL_BWD_NOSM
         else
           bwd_softmax_grad<false>(sacc, dp, dl, mwr, a.T, mykey, mw_bit, qsub0 + 4 * h32);
+#endif
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
           const bf16x8 pf = pack_frag(sacc, st);
           const bf16x8 dsf = pack_frag(dp, st);
           const int rb = (qs * 32 + 16 * st) * ROWB;  // 16-row aligned: an immediate
+#ifdef MG_ABL_BWD_NOKV
+          dv[0][st] += __builtin_bit_cast(float, __builtin_bit_cast(uint4, pf).x ^ __builtin_bit_cast(uint4, dsf).y);
+          continue;
+#endif
 #pragma unroll
           for (int n = 0; n < NO; ++n) {
             const int hb = (n >> 1) * HQ + rb;
@@ -434,6 +449,10 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
         }
       }
       __syncthreads();  // dS of all KB keys in LDS
+      // the next tile's Q / dO / row constants / keep words into LDS now: the dQ products below
+      // read only dS^T and K, and committing before the dQ stores keeps the wait for this tile's
+      // loads (and any spill reload there) from draining those stores
+      if (more) commit(qt + 1);
       // dQ[BQ q][hd] = dS[BQ q][KB keys] (c K)[KB keys][hd]
 #pragma unroll
       for (int i = 0; i < NTW; ++i) {
@@ -478,6 +497,9 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
           }
         }
         const int d = n * 32 + l32;
+#ifdef MG_ABL_BWD_NODQST
+        if (dq[0] == 12345.f)
+#endif
         if (my_split == 0 && d < a.hd && qbase + qs * 32 + 31 >= kb0) {
           if (PERSIST && !first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
           // row q0 + (r & 3) + 8 (r >> 2): one 64-bit base per lane, then uniform row strides
@@ -503,7 +525,6 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
           }
         }
       }
-      if (more) commit(qt + 1);
       __syncthreads();
     }
 

@@ -92,7 +92,12 @@ struct GemmArgs {
 static unsigned long long* g_dbg = nullptr;  // MG_GEMM_STAMPS builds: stamp buffer
 static int g_variant = 0;  // 0 auto, 1 force T128, 2 force T256, 3 force T2x1, 4 force PP, 5 force W4, 6 force W4 BN=192
 
-MG_DEVICE int swz_mn(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+// Chunk swizzle of the m/n-contiguous [64 k][256 B] half-images: rows 8 g + q (q < 4) of one
+// transposed read get 8 distinct chunk pairs (conflict-free ds_read_b64_tr_b16), and bit 2 of the
+// row is not used, so row r + 4 -- the second read of a fragment -- is the first one's address +
+// 1024 (an immediate offset: no address VALU, which overflowed the MFMA gaps of the weight-gradient
+// main loop: 1.54k vs 1.02k cycles per phase, tools/gemm_stamps.hip layout 2)
+MG_DEVICE int swz_mn(int r) { return ((r & 3) << 2) | (((r >> 3) & 1) << 1); }
 
 // ---- Buffer descriptor of K-tile t: base advanced to the tile's first k, extent shrunk with it,
 // so per-lane offsets stay fixed while out-of-range rows (kOOB) and the buffer end still read 0.
@@ -192,6 +197,14 @@ MG_DEVICE s16x4 ds_read_tr16(const char* p) {
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_addr(p)));
   return r;
 }
+// the same with a constant byte offset in the instruction's offset field (no address VALU)
+template <int OFF>
+MG_DEVICE s16x4 ds_read_tr16_off(uint32_t addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
 template <int N>
 MG_DEVICE void lds_ready(bf16x8 (&f)[N], bool wait = true) {
   if (wait) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -212,9 +225,29 @@ MG_DEVICE bf16x8 frag(const char* lds, int sb, int ks, int lane) {
     const int chk = (sb & 7) * 2 + (p >> 1);
     const int r0 = ks * 32 + 8 * g + q, r1 = r0 + 4;
     const char* a0 = img + r0 * 256 + ((chk ^ swz_mn(r0)) << 4) + (p & 1) * 8;
-    const char* a1 = img + r1 * 256 + ((chk ^ swz_mn(r1)) << 4) + (p & 1) * 8;
+    const char* a1 = a0 + (r1 - r0) * 256;  // swz_mn(r0 + 4) == swz_mn(r0)
     const s16x4 x = ds_read_tr16(a0);
     const s16x4 y = ds_read_tr16(a1);
+    const s16x8 v = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+// frag with the k-step a template constant (W4): for m/n-contiguous images the k-step and the
+// fragment's second row group go into the transposed reads' offset fields, so a fragment costs one
+// address add (the ring slot base) and two reads
+template <bool KC, int KS>
+MG_DEVICE bf16x8 frag_k(const char* lds, int sb, int lane) {
+  if constexpr (KC) {
+    return frag<true>(lds, sb, KS, lane);
+  } else {
+    const char* img = lds + (sb >> 3) * 16384;
+    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    const int chk = (sb & 7) * 2 + (p >> 1);
+    const int r0 = 8 * g + q;  // + 32 KS (swz_mn ignores bits 2 and 5 of the row)
+    const uint32_t a = lds_addr(img + r0 * 256 + ((chk ^ swz_mn(r0)) << 4) + (p & 1) * 8);
+    const s16x4 x = ds_read_tr16_off<KS * 32 * 256>(a);
+    const s16x4 y = ds_read_tr16_off<KS * 32 * 256 + 4 * 256>(a);
     const s16x8 v = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
     return __builtin_bit_cast(bf16x8, v);
   }
@@ -1177,9 +1210,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
 
   bf16x8 fa0[8], fb0[FN], fa1[8], fb1[FN];
 #pragma unroll
-  for (int j = 0; j < FN; ++j) fb0[j] = frag<BKC>(sB, wn * FN + j, 0, lane);
+  for (int j = 0; j < FN; ++j) fb0[j] = frag_k<BKC, 0>(sB, wn * FN + j, lane);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) fa0[i] = frag<AK>(smem, wm * 8 + i, 0, lane);
+  for (int i = 0; i < 8; ++i) fa0[i] = frag_k<AK, 0>(smem, wm * 8 + i, lane);
   lds_ready(fa0);
   lds_ready(fb0, false);
   W4_STAMP(7);
@@ -1204,8 +1237,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
         if ((q & 1) == 0 && q < 2 * NR) {
           // B fragments first: the next phase's first FN MFMAs use fa[0] with every fb[j]
           const int r = q >> 1;
-          if (r < FN) fb1[r] = frag<BKC>(sb, wn * FN + r, 1, lane);
-          else fa1[r - FN] = frag<AK>(sa, wm * 8 + r - FN, 1, lane);
+          if (r < FN) fb1[r] = frag_k<BKC, 1>(sb, wn * FN + r, lane);
+          else fa1[r - FN] = frag_k<AK, 1>(sa, wm * 8 + r - FN, lane);
         }
         if (w4_piece_at<NQ, WK::PB>(q) >= 0) stb.piece(dstb, rb, tt, w4_piece_at<NQ, WK::PB>(q), false);
       }
@@ -1239,8 +1272,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
           // fragment reads of tile kt+1 step 0, B first, early in the phase so they have ~3/4 of
           // it to land before the next phase A needs them
           const int r = q >> 1;
-          if (r < FN) fb0[r] = frag<BKC>(snb, wn * FN + r, 0, lane);
-          else fa0[r - FN] = frag<AK>(sn, wm * 8 + r - FN, 0, lane);
+          if (r < FN) fb0[r] = frag_k<BKC, 0>(snb, wn * FN + r, lane);
+          else fa0[r - FN] = frag_k<AK, 0>(sn, wm * 8 + r - FN, lane);
         }
       }
     }

@@ -1,5 +1,6 @@
 // gemm_stamps: diagnostic build of the GEMM kernels with per-phase s_memtime stamps.
-// Runs one M x N x K NT GEMM (random bf16) under a forced tile config and prints, per phase of
+// Runs one M x N x K GEMM (random bf16; layout 0 = NT forward, 2 = TN weight gradient: fp32
+// split-K accumulate, K = tokens) under a forced tile config and prints, per phase of
 // the ping-pong kernel's K-tile MG_GEMM_STAMPS, the median cycles of each segment over all waves:
 //   reads+DMA issue | vmcnt wait | barrier 1 | lgkmcnt wait | MFMA | barrier 2 (next phase start)
 // Build: hipcc --offload-arch=gfx950 -O3 -DMG_GEMM_STAMPS=20 -Icsrc/include tools/gemm_stamps.hip
@@ -18,7 +19,8 @@ const uint64_t* graph_seed_ofs() { return nullptr; }  // eager launches only (ad
 
 int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 8192, N = argc > 2 ? atoi(argv[2]) : 8192,
-            K = argc > 3 ? atoi(argv[3]) : 8192, variant = argc > 4 ? atoi(argv[4]) : 4;
+            K = argc > 3 ? atoi(argv[3]) : 8192, variant = argc > 4 ? atoi(argv[4]) : 4,
+            layout = argc > 5 ? atoi(argv[5]) : 0;
   std::vector<uint16_t> ha((size_t)M * K), hb((size_t)N * K);
   std::mt19937 rng(1);
   std::uniform_int_distribution<int> d(0, 0x7f);
@@ -28,16 +30,22 @@ int main(int argc, char** argv) {
   unsigned long long* dbg;
   hipMalloc(&a, ha.size() * 2);
   hipMalloc(&b, hb.size() * 2);
-  hipMalloc(&c, (size_t)M * N * 2);
-  const int blocks = cdiv(M, 256) * cdiv(N, 256);
+  hipMalloc(&c, (size_t)M * N * (layout == 2 ? 4 : 2));
+  hipMemset(c, 0, (size_t)M * N * (layout == 2 ? 4 : 2));
+  // blocks with stamp slots: output tiles x split-K chunks (at most 64 splits)
+  const int blocks = cdiv(M, 256) * cdiv(N, 256) * (layout == 2 ? 64 : 1);
   hipMalloc(&dbg, (size_t)blocks * 8 * 24 * 8);
   hipMemset(dbg, 0, (size_t)blocks * 8 * 24 * 8);
   hipMemcpy(a, ha.data(), ha.size() * 2, hipMemcpyHostToDevice);
   hipMemcpy(b, hb.data(), hb.size() * 2, hipMemcpyHostToDevice);
   mg::gemm_set_variant(variant);
   auto run = [&] {
-    mg::gemm(0, 0, a, b, c, K, K, N, M, N, K, M, N, K, K, nullptr, nullptr, nullptr, 0.f, 0, 0,
-             (size_t)M * K * 2, (size_t)N * K * 2);
+    if (layout == 2)  // C[M, N] += A[K, M]^T B[K, N]
+      mg::gemm(2, 0, a, b, c, M, N, N, M, N, K, M, N, K, K, nullptr, nullptr, nullptr, 0.f, 0, 0,
+               (size_t)M * K * 2, (size_t)N * K * 2);
+    else
+      mg::gemm(0, 0, a, b, c, K, K, N, M, N, K, M, N, K, K, nullptr, nullptr, nullptr, 0.f, 0, 0,
+               (size_t)M * K * 2, (size_t)N * K * 2);
   };
   for (int i = 0; i < 3; ++i) run();
   hipEvent_t e0, e1;
@@ -49,7 +57,8 @@ int main(int argc, char** argv) {
   hipEventSynchronize(e1);
   float ms;
   hipEventElapsedTime(&ms, e0, e1);
-  printf("variant %d  %dx%dx%d: %.3f ms  %.1f TF/s\n", variant, M, N, K, ms / 5, 2.0 * M * N * K / (ms / 5 * 1e-3) / 1e12);
+  printf("variant %d layout %d  %dx%dx%d: %.3f ms  %.1f TF/s\n", variant, layout, M, N, K, ms / 5,
+         2.0 * M * N * K / (ms / 5 * 1e-3) / 1e12);
   mg::gemm_set_debug_buffer(dbg);
   run();
   hipDeviceSynchronize();
