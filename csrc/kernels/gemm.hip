@@ -778,10 +778,13 @@ __global__ __launch_bounds__(CF::NT, 2) void gemm_kernel(const GemmArgs args) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 fa[CF::FM], fb[CF::FN];
+      // k-step as a template constant (frag_k: offset-field transposed reads)
 #pragma unroll
-      for (int i = 0; i < CF::FM; ++i) fa[i] = frag<AK>(sa, wm * CF::FM + i, ks, lane);
+      for (int i = 0; i < CF::FM; ++i)
+        fa[i] = ks ? frag_k<AK, 1>(sa, wm * CF::FM + i, lane) : frag_k<AK, 0>(sa, wm * CF::FM + i, lane);
 #pragma unroll
-      for (int j = 0; j < CF::FN; ++j) fb[j] = frag<BKC>(sb, wn * CF::FN + j, ks, lane);
+      for (int j = 0; j < CF::FN; ++j)
+        fb[j] = ks ? frag_k<BKC, 1>(sb, wn * CF::FN + j, lane) : frag_k<BKC, 0>(sb, wn * CF::FN + j, lane);
       if constexpr (!AK || !BKC) {
         lds_ready(fa);
         lds_ready(fb, false);

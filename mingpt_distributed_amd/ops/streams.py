@@ -40,12 +40,12 @@ from typing import Callable, Deque, Dict, Tuple
 import torch
 
 # "auto" (default): the side stream for weight gradients over at most _AUTO_TOKENS rows (tokens),
-# where their tiles underfill the GPU -- measured on one box (profiles/round4_wgrad_stream_ab.txt):
-# gpt2-xl at 16k tokens +1.2 %, GPT-2 at 131k tokens -1.1 % (its weight gradients already fill
-# the chip; the concurrency only adds contention).  "1" always, "0" never.
+# where their tiles underfill the GPU -- measured on one box each (profiles/round4_wgrad_stream_ab.txt):
+# gpt2-xl at 16k tokens +1.2 %, at 32k tokens -3.3 %, GPT-2 at 131k tokens -1.1 % (those weight
+# gradients fill the chip already; the concurrency only adds contention).  "1" always, "0" never.
 _MODE = os.environ.get("MINGPT_WGRAD_STREAM", "auto").lower()
 _ENABLED = _MODE != "0"
-_AUTO_TOKENS = int(os.environ.get("MINGPT_WGRAD_STREAM_TOKENS", "32768"))
+_AUTO_TOKENS = int(os.environ.get("MINGPT_WGRAD_STREAM_TOKENS", "16384"))
 # weight gradients in flight before the compute stream waits for the oldest (4 = one block)
 _LAG = max(1, int(os.environ.get("MINGPT_WGRAD_LAG", "4")))
 _side: Dict[int, "torch.cuda.Stream"] = {}

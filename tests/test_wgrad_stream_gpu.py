@@ -57,4 +57,4 @@ def test_side_stream_training_steps_reduce_loss():
 
 def test_auto_mode_picks_small_weight_gradients():
     streams.set_enabled(True, "auto")
-    assert streams.use_for(16384) and not streams.use_for(131072)
+    assert streams.use_for(16384) and not streams.use_for(32768) and not streams.use_for(131072)

@@ -1,5 +1,5 @@
 // gemm_stamps: diagnostic build of the GEMM kernels with per-phase s_memtime stamps.
-// Runs one M x N x K GEMM (random bf16; layout 0 = NT forward, 2 = TN weight gradient: fp32
+// Runs one M x N x K GEMM (random bf16; layout 0 = NT forward, 1 = NN data gradient, 2 = TN weight gradient: fp32
 // split-K accumulate, K = tokens) under a forced tile config and prints, per phase of
 // the ping-pong kernel's K-tile MG_GEMM_STAMPS, the median cycles of each segment over all waves:
 //   reads+DMA issue | vmcnt wait | barrier 1 | lgkmcnt wait | MFMA | barrier 2 (next phase start)
@@ -42,6 +42,9 @@ int main(int argc, char** argv) {
   auto run = [&] {
     if (layout == 2)  // C[M, N] += A[K, M]^T B[K, N]
       mg::gemm(2, 0, a, b, c, M, N, N, M, N, K, M, N, K, K, nullptr, nullptr, nullptr, 0.f, 0, 0,
+               (size_t)M * K * 2, (size_t)N * K * 2);
+    else if (layout == 1)  // data gradient: C[M, N] = A[M, K] B[K, N]
+      mg::gemm(1, 0, a, b, c, K, N, N, M, N, K, M, N, K, K, nullptr, nullptr, nullptr, 0.f, 0, 0,
                (size_t)M * K * 2, (size_t)N * K * 2);
     else
       mg::gemm(0, 0, a, b, c, K, K, N, M, N, K, M, N, K, K, nullptr, nullptr, nullptr, 0.f, 0, 0,
