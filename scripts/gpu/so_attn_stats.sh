@@ -7,11 +7,14 @@ set -o pipefail
 cd "$(dirname "$0")/../.."
 TAG=$1; ROUNDS=$2; shift 2
 OUT=gpurun_out/$TAG; mkdir -p "$OUT"; export TMPDIR=/tmp
+# an entry may carry one environment setting: so@VAR=VALUE (e.g. tree@MINGPT_ATTN_FWD_DPV=0)
 for r in $(seq 1 "$ROUNDS"); do
-  for so in "$@"; do
+  for ent in "$@"; do
+    so=${ent%%@*}; ev=""; [ "$ent" != "$so" ] && ev=${ent#*@}
     n=$(basename "$(dirname "$so")"); [ "$so" = tree ] && n=tree
+    [ -n "$ev" ] && n="${n}_$(echo "$ev" | tr '=' '_')"
     if [ "$so" = tree ]; then unset MINGPT_EXT_SO; else export MINGPT_EXT_SO=$so; fi
-    timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${n}_$r" -o run -- \
+    env $ev timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${n}_$r" -o run -- \
       python3 bench/dev/attn_prof.py > "$OUT/${n}_$r.log" 2>&1 || { tail -20 "$OUT/${n}_$r.log"; exit 1; }
     f=$(find "$OUT/${n}_$r" -name '*kernel_stats.csv' | head -1)
     python3 - "$f" "$n" "$r" <<'PY'
