@@ -30,6 +30,11 @@
 //    LDS-staged atomics.
 #include "common.h"
 #include "kernels.h"
+#include <type_traits>
+
+#ifndef MG_W4_UNROLL
+#define MG_W4_UNROLL 1  // W4 K-loop unrolled over the ring-slot pattern for m/n-contiguous operands
+#endif
 
 using namespace mg;
 
@@ -115,7 +120,9 @@ MG_DEVICE __amdgpu_buffer_rsrc_t tile_rsrc(const char* base, uint32_t bytes, uin
 // Each buffer_load ... lds wave-instruction writes 1 KiB at (wave-uniform base + lane*16).
 // Per-lane source offsets are computed once; a K-tile costs one descriptor (SALU) plus, per piece,
 // an M0 write and the load.  Per-lane k checks run only on K-tiles that cross the valid k extent.
-template <bool KC, int R, int NW>
+// HS: byte stride between the two 128-column half-images of an m/n-contiguous operand (16 KiB:
+// contiguous halves; W4's slot-unrolled loop interleaves the ring's slots inside each half)
+template <bool KC, int R, int NW, int HS = 16384>
 struct Stager {
   static constexpr int PER = R / 8 / NW;  // 1-KiB pieces per wave (R*128 B per tile)
   uint32_t voff[PER];
@@ -174,7 +181,8 @@ struct Stager {
       const int kpos = KC ? ((lane & 7) ^ ((lane >> 3) & 7)) * 8 : 4 * (j & 15) + (lane >> 4);
       off = kpos < klim - t * BK ? off : kOOB;
     }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + j * 1024), 16, off, 0, 0, 0);
+    char* dst = KC ? lds + j * 1024 : lds + (j >> 4) * HS + (j & 15) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)dst, 16, off, 0, 0, 0);
   }
   MG_DEVICE void stage(char* lds, int t) const {
     const __amdgpu_buffer_rsrc_t rs = tile_rsrc(base, bytes, step, t);
@@ -236,18 +244,20 @@ MG_DEVICE bf16x8 frag(const char* lds, int sb, int ks, int lane) {
 // frag with the k-step a template constant (W4): for m/n-contiguous images the k-step and the
 // fragment's second row group go into the transposed reads' offset fields, so a fragment costs one
 // address add (the ring slot base) and two reads
-template <bool KC, int KS>
+// HS: half-image stride; OFF: a constant byte offset (W4's slot-unrolled loop: the ring slot) that
+// also goes into the offset field
+template <bool KC, int KS, int HS = 16384, int OFF = 0>
 MG_DEVICE bf16x8 frag_k(const char* lds, int sb, int lane) {
   if constexpr (KC) {
-    return frag<true>(lds, sb, KS, lane);
+    return frag<true>(lds + OFF, sb, KS, lane);
   } else {
-    const char* img = lds + (sb >> 3) * 16384;
+    const char* img = lds + (sb >> 3) * HS;
     const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
     const int chk = (sb & 7) * 2 + (p >> 1);
     const int r0 = 8 * g + q;  // + 32 KS (swz_mn ignores bits 2 and 5 of the row)
     const uint32_t a = lds_addr(img + r0 * 256 + ((chk ^ swz_mn(r0)) << 4) + (p & 1) * 8);
-    const s16x4 x = ds_read_tr16_off<KS * 32 * 256>(a);
-    const s16x4 y = ds_read_tr16_off<KS * 32 * 256 + 4 * 256>(a);
+    const s16x4 x = ds_read_tr16_off<OFF + KS * 32 * 256>(a);
+    const s16x4 y = ds_read_tr16_off<OFF + KS * 32 * 256 + 4 * 256>(a);
     const s16x8 v = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
     return __builtin_bit_cast(bf16x8, v);
   }
@@ -1190,8 +1200,14 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
 
   const int kbeg = split * args.kchunk;
   const int nk = (min(args.K, kbeg + args.kchunk) - kbeg + BK - 1) / BK;
-  Stager<AK, 256, 4> sta;
-  Stager<BKC, BN, 4> stb;
+  // m/n-contiguous operands (the data and weight gradients): the ring's slots interleaved inside
+  // each 128-column half-image (16 KiB per slot and half), so that with the K-loop unrolled over
+  // the slot pattern every transposed read's slot offset is a constant in its offset field
+  constexpr bool UNR = MG_W4_UNROLL && (!AK || !BKC);
+  constexpr int AS = AK ? WK::A_SLOT : 16384, AHS = 2 * 16384;  // A: slot / half-image strides
+  constexpr int BS = BKC ? WK::B_SLOT : 16384, BHS = 3 * 16384;  // B: 3 slots
+  Stager<AK, 256, 4, AHS> sta;
+  Stager<BKC, BN, 4, BHS> stb;
   sta.init(args.A, args.a_bytes, args.lda, m0, args.a_ext, kbeg, args.ka, kbeg + args.kchunk, wid, lane);
   stb.init(args.B, args.b_bytes, args.ldb, n0, args.b_ext, kbeg, args.kb, kbeg + args.kchunk, wid, lane);
   // K-tile visiting order: a partial last K-tile (K % 64 != 0; W4 layouts have ka = kb = K and
@@ -1202,8 +1218,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
   sta.stage(smem, w4_tile(0, nk, tail_first));
   stb.stage(sB, w4_tile(0, nk, tail_first));
   if (nk > 1) {
-    sta.stage(smem + WK::A_SLOT, w4_tile(1, nk, tail_first));
-    stb.stage(sB + WK::B_SLOT, w4_tile(1, nk, tail_first));
+    sta.stage(smem + AS, w4_tile(1, nk, tail_first));
+    stb.stage(sB + BS, w4_tile(1, nk, tail_first));
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WK::PA + WK::PB) : "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1213,15 +1229,87 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
 
   bf16x8 fa0[8], fb0[FN], fa1[8], fb1[FN];
 #pragma unroll
-  for (int j = 0; j < FN; ++j) fb0[j] = frag_k<BKC, 0>(sB, wn * FN + j, lane);
+  for (int j = 0; j < FN; ++j) fb0[j] = frag_k<BKC, 0, BHS>(sB, wn * FN + j, lane);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) fa0[i] = frag_k<AK, 0>(smem, wm * 8 + i, lane);
+  for (int i = 0; i < 8; ++i) fa0[i] = frag_k<AK, 0, AHS>(smem, wm * 8 + i, lane);
   lds_ready(fa0);
   lds_ready(fb0, false);
   W4_STAMP(7);
 
+  // One K-tile with compile-time ring slots SA (A, kt & 1) and SB (B, kt % 3): the same schedule
+  // as the runtime-slot loop below (see it for the phase comments)
+  auto ktile = [&](int kt, auto sa_c, auto sb_c) __attribute__((always_inline)) {
+    constexpr int SA = decltype(sa_c)::value, SB = decltype(sb_c)::value;
+    constexpr int OA = SA * AS, OA1 = (SA ^ 1) * AS;
+    constexpr int OB = SB * BS, OB1 = ((SB + 1) % 3) * BS, OB2 = ((SB + 2) % 3) * BS;
+    W4_KSTAMP(0);
+    const int t2 = kt + 2;
+    const int tt = w4_tile(t2 < nk ? t2 : 1, nk, tail_first);
+    {
+      const __amdgpu_buffer_rsrc_t rb = stb.rsrc(tt);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int i = q / FN, j = q % FN;
+        mfma_acc(acc[i][j], fb0[j], fa0[i]);
+        if ((q & 1) == 0 && q < 2 * NR) {
+          const int r = q >> 1;
+          if (r < FN) fb1[r] = frag_k<BKC, 1, BHS, OB>(sB, wn * FN + r, lane);
+          else fa1[r - FN] = frag_k<AK, 1, AHS, OA>(smem, wm * 8 + r - FN, lane);
+        }
+        if (w4_piece_at<NQ, WK::PB>(q) >= 0) stb.piece(sB + OB2, rb, tt, w4_piece_at<NQ, WK::PB>(q), false);
+      }
+    }
+    W4_KSTAMP(1);
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(WK::PB) : "memory");
+    lds_ready(fa1, false);
+    lds_ready(fb1, false);
+    W4_KSTAMP(2);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    W4_KSTAMP(3);
+    {
+      const __amdgpu_buffer_rsrc_t ra = sta.rsrc(tt);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int i = q / FN, j = q % FN;
+        if (q == NQ - 1) mfma_acc_last(acc[i][j], fb1[j], fa1[i]);
+        else mfma_acc(acc[i][j], fb1[j], fa1[i]);
+        if (w4_piece_at<NQ, WK::PA>(q) >= 0) sta.piece(smem + OA, ra, tt, w4_piece_at<NQ, WK::PA>(q), false);
+        if (q < 2 * NR && (q & 1) == 1) {
+          const int r = q >> 1;
+          if (r < FN) fb0[r] = frag_k<BKC, 0, BHS, OB1>(sB, wn * FN + r, lane);
+          else fa0[r - FN] = frag_k<AK, 0, AHS, OA1>(smem, wm * 8 + r - FN, lane);
+        }
+      }
+    }
+    W4_KSTAMP(4);
+    lds_ready(fa0);
+    lds_ready(fb0, false);
+    W4_KSTAMP(5);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+
+  if constexpr (UNR) {
+    // slot pattern of K-tiles 6n .. 6n + 5: (A, B) = (0,0) (1,1) (0,2) (1,0) (0,1) (1,2)
+    int kt = 0;
+    for (; kt + 6 <= nk; kt += 6) {
+      ktile(kt, I0{}, I0{});
+      ktile(kt + 1, I1{}, I1{});
+      ktile(kt + 2, I0{}, I2{});
+      ktile(kt + 3, I1{}, I0{});
+      ktile(kt + 4, I0{}, I1{});
+      ktile(kt + 5, I1{}, I2{});
+    }
+    if (kt < nk) ktile(kt, I0{}, I0{});
+    if (kt + 1 < nk) ktile(kt + 1, I1{}, I1{});
+    if (kt + 2 < nk) ktile(kt + 2, I0{}, I2{});
+    if (kt + 3 < nk) ktile(kt + 3, I1{}, I0{});
+    if (kt + 4 < nk) ktile(kt + 4, I0{}, I1{});
+  }
   int bs = 0;  // B slot of tile kt (kt % 3)
-  for (int kt = 0; kt < nk; ++kt) {
+  for (int kt = 0; kt < (UNR ? 0 : nk); ++kt) {
     W4_KSTAMP(0);
     const int bs1 = bs == 2 ? 0 : bs + 1, bs2 = bs == 0 ? 2 : bs - 1;  // slots of kt+1, kt+2
     const char* sa = smem + (kt & 1) * WK::A_SLOT;
