@@ -500,7 +500,18 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
 #ifdef MG_ABL_BWD_NODQST
         if (dq[0] == 12345.f)
 #endif
-        if (my_split == 0 && d < a.hd && qbase + qs * 32 + 31 >= kb0) {
+        if (part && my_split == 0 && d < a.hd && qbase + qs * 32 + 31 >= kb0) {
+          // key-block partial: buffer stores through one descriptor per query tile whose extent
+          // ends at row T of this sequence (rows past it are dropped: no per-row branches), row
+          // offsets in SGPRs (no 64-bit address math per store)
+          const uint64_t org = ((uint64_t)kb * a.dq_part + ((uint64_t)b * a.T + qbase) * a.D + (uint64_t)hh * a.hd) * 4;
+          const uint64_t end = ((uint64_t)kb * a.dq_part + ((uint64_t)b + 1) * a.T * a.D) * 4;
+          const __amdgpu_buffer_rsrc_t rs = kv_rsrc(reinterpret_cast<const bf16_t*>(a.dq), end, org);
+          const int voff = ((qs * 32 + 4 * h32) * a.D + d) * 4;
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dq[r]), rs, voff, ((r & 3) + 8 * (r >> 2)) * a.D * 4, 0);
+        } else if (my_split == 0 && d < a.hd && qbase + qs * 32 + 31 >= kb0) {
           if (PERSIST && !first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
           // row q0 + (r & 3) + 8 (r >> 2): one 64-bit base per lane, then uniform row strides
           const int q0 = qbase + qs * 32 + 4 * h32;
