@@ -230,7 +230,7 @@ void adamw_step(const at::Tensor& chunk_start, const at::Tensor& chunk_len,
                 const at::Tensor& master, const at::Tensor& param, const at::Tensor& grad,
                 const at::Tensor& m, const at::Tensor& v, const at::Tensor& norm, double lr,
                 double b1, double b2, double eps, int64_t step, double grad_scale, double clip,
-                int64_t table_end, int64_t moment_end) {
+                int64_t table_end, int64_t moment_end, const c10::optional<at::Tensor>& zero_grad) {
   CHECK_I64(chunk_start); CHECK_DEV(chunk_len); CHECK_F32(chunk_wd);
   TORCH_CHECK(chunk_len.scalar_type() == at::kInt, "chunk_len must be int32");
   CHECK_F32(master); CHECK_BF16(param); CHECK_F32(m); CHECK_F32(v); CHECK_F32(norm);
@@ -253,12 +253,19 @@ void adamw_step(const at::Tensor& chunk_start, const at::Tensor& chunk_len,
     TORCH_CHECK(m.numel() == n && v.numel() == n, "adamw: moment buffer size mismatch");
   }
   TORCH_CHECK(chunk_start.numel() == chunk_len.numel() && chunk_wd.numel() == chunk_len.numel());
+  float* zg = nullptr;  // fp32 main grads zeroed as they are consumed (same flat indexing)
+  if (zero_grad.has_value() && zero_grad->defined()) {
+    CHECK_F32(*zero_grad);
+    TORCH_CHECK(zero_grad->numel() >= table_end, "adamw: zero_grad buffer shorter than the chunk table");
+    zg = fp(*zero_grad);
+  }
   if (chunk_len.numel() == 0) return;
   DevGuard g(master.device());
   mg::adamw_step(chunk_start.data_ptr<int64_t>(), chunk_len.data_ptr<int>(), fp(chunk_wd), ms,
                  (int)chunk_len.numel(), fp(master), bp(param), grad.data_ptr(),
                  grad.scalar_type() == at::kBFloat16, fp(m), fp(v), fp(norm), (float)lr, (float)b1,
-                 (float)b2, (float)eps, (int)step, (float)grad_scale, (float)clip, cur_stream());
+                 (float)b2, (float)eps, (int)step, (float)grad_scale, (float)clip, cur_stream(),
+                 zg);
 }
 
 void f32_to_bf16(const at::Tensor& src, const at::Tensor& dst) {
@@ -666,7 +673,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_graph_state", &set_graph_state, py::arg("seed_ofs") = py::none(), py::arg("opt_hp") = py::none());
   m.def("grad_sumsq", &grad_sumsq);
   m.def("grad_sumsq_chunks", &grad_sumsq_chunks);
-  m.def("adamw_step", &adamw_step);
+  m.def("adamw_step", &adamw_step, py::arg("chunk_start"), py::arg("chunk_len"), py::arg("chunk_wd"),
+        py::arg("moment_start"), py::arg("master"), py::arg("param"), py::arg("grad"), py::arg("m"),
+        py::arg("v"), py::arg("norm"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"),
+        py::arg("step"), py::arg("grad_scale"), py::arg("clip"), py::arg("table_end"),
+        py::arg("moment_end"), py::arg("zero_grad") = py::none());
   m.def("f32_to_bf16", &f32_to_bf16);
   m.def("bias_act", &bias_act);
   m.def("bias_dropout_residual", &bias_dropout_residual);

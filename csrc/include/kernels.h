@@ -54,7 +54,7 @@ void adamw_step(const int64_t* chunk_start, const int* chunk_len, const float* c
                 const int64_t* moment_start, int n_chunks, float* master, bf16_t* param,
                 const void* grad, bool grad_bf16, float* m, float* v, const float* norm, float lr,
                 float b1, float b2, float eps, int step, float grad_scale, float clip,
-                hipStream_t stream);
+                hipStream_t stream, float* zero_grad = nullptr);
 void f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t stream);
 
 // gemv.hip (decode-time skinny GEMM, B <= 8 rows; epi 0 none, 1 bias, 2 bias+GELU, 3 bias+residual)

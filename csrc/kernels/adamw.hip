@@ -99,6 +99,8 @@ __global__ __launch_bounds__(256) void sumsq_chunks_kernel(const int64_t* __rest
 // chunk b updates master/param/grad[chunk_start[b] ...] and the moments at
 // m/v[moment_start[b] ...] (moment_start == nullptr: the same index).  Replicated DP keeps
 // moments for the whole flat buffer; ZeRO-1 keeps them only for the rank's pieces, packed.
+// zg (optional): the fp32 main-grad buffer, zeroed at each updated element once read (the
+// separate zero-fill pass fused in: the same bytes, one launch fewer).
 template <typename G>
 __global__ __launch_bounds__(256) void adamw_kernel(
     const int64_t* __restrict__ chunk_start, const int* __restrict__ chunk_len,
@@ -106,24 +108,25 @@ __global__ __launch_bounds__(256) void adamw_kernel(
     float* __restrict__ master, bf16_t* __restrict__ param, const G* __restrict__ grad,
     float* __restrict__ m, float* __restrict__ v, const float* __restrict__ norm, float lr, float b1,
     float b2, float eps, float bc1, float bc2_sqrt, float grad_scale, float clip,
-    const float* __restrict__ hp) {
+    const float* __restrict__ hp, int n_chunks, float* __restrict__ zg) {
   if (hp) {  // graph mode: {lr, step} from device memory (the host values were captured once)
     lr = hp[0];
     bc1 = 1.f - powf(b1, hp[1]);
     bc2_sqrt = sqrtf(1.f - powf(b2, hp[1]));
   }
-  const long s0 = chunk_start[blockIdx.x];
-  const long ms0 = moment_start ? moment_start[blockIdx.x] : s0;
-  const int len = chunk_len[blockIdx.x];
-  const float wd = chunk_wd[blockIdx.x];
   float gs = grad_scale;
   if (clip > 0.f) {
     const float tn = sqrtf(norm[0]) * grad_scale;
     const float coef = clip / (tn + 1e-6f);
     if (coef < 1.f) gs *= coef;
   }
-  const float decay = 1.f - lr * wd;
   const float step = lr / bc1;
+  const float z4[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+  const long s0 = chunk_start[c];
+  const long ms0 = moment_start ? moment_start[c] : s0;
+  const int len = chunk_len[c];
+  const float decay = 1.f - lr * chunk_wd[c];
   // every operand is touched once per step: non-temporal loads / stores (no L2 / MALL pollution),
   // and two float4 groups per thread per iteration so 8 loads are in flight before any use
   auto upd = [&](float (&pa)[4], const float (&ga)[4], float (&ma)[4], float (&va)[4]) {
@@ -150,6 +153,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(
     for (int u = 0; u < 2; ++u) {
       const long e = s0 + i + u * 1024, me = ms0 + i + u * 1024;
       upd(pa[u], ga[u], ma[u], va[u]);
+      if (zg) st4_nt(zg + e, z4);  // after the grad's use: its load has returned
       st4_nt(master + e, pa[u]);
       st4_nt(m + me, ma[u]);
       st4_nt(v + me, va[u]);
@@ -167,6 +171,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(
       ld4_nt(m + me, ma);
       ld4_nt(v + me, va);
       upd(pa, ga, ma, va);
+      if (zg) st4_nt(zg + e, z4);
       st4_nt(master + e, pa);
       st4_nt(m + me, ma);
       st4_nt(v + me, va);
@@ -175,6 +180,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(
       for (int j = 0; j < 4 && i + j < len; ++j) {
         const long k = e + j, mk = me + j;
         const float gg = load_grad1(grad, k) * gs;
+        if (zg) zg[k] = 0.f;
         const float mj = b1 * m[mk] + (1.f - b1) * gg;
         const float vj = b2 * v[mk] + (1.f - b2) * gg * gg;
         const float pj = master[k] * decay - step * mj / (sqrtf(vj) / bc2_sqrt + eps);
@@ -184,6 +190,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(
         param[k] = f2bf(pj);
       }
     }
+  }
   }
 }
 
@@ -232,19 +239,20 @@ void adamw_step(const int64_t* chunk_start, const int* chunk_len, const float* c
                 const int64_t* moment_start, int n_chunks, float* master, bf16_t* param,
                 const void* grad, bool grad_bf16, float* m, float* v, const float* norm, float lr,
                 float b1, float b2, float eps, int step, float grad_scale, float clip,
-                hipStream_t stream) {
+                hipStream_t stream, float* zero_grad) {
   const float bc1 = 1.f - powf(b1, (float)step);
   const float bc2_sqrt = sqrtf(1.f - powf(b2, (float)step));
+  const int grid = n_chunks;  // one workgroup per chunk
   if (grad_bf16)
-    adamw_kernel<bf16_t><<<n_chunks, 256, 0, stream>>>(
+    adamw_kernel<bf16_t><<<grid, 256, 0, stream>>>(
         chunk_start, chunk_len, chunk_wd, moment_start, master, param,
         static_cast<const bf16_t*>(grad), m, v, norm, lr, b1, b2, eps, bc1, bc2_sqrt, grad_scale,
-        clip, g_opt_hp);
+        clip, g_opt_hp, n_chunks, zero_grad);
   else
-    adamw_kernel<float><<<n_chunks, 256, 0, stream>>>(
+    adamw_kernel<float><<<grid, 256, 0, stream>>>(
         chunk_start, chunk_len, chunk_wd, moment_start, master, param,
         static_cast<const float*>(grad), m, v, norm, lr, b1, b2, eps, bc1, bc2_sqrt, grad_scale,
-        clip, g_opt_hp);
+        clip, g_opt_hp, n_chunks, zero_grad);
 }
 
 void f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t stream) {

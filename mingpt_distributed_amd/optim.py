@@ -237,7 +237,9 @@ class FusedAdamW:
         """Global grad norm of the last step (device tensor; read it lazily)."""
         return self.norm_buf[1]
 
-    def step(self, grad_scale: float = 1.0, lr: Optional[float] = None):
+    def step(self, grad_scale: float = 1.0, lr: Optional[float] = None, zero_grad: bool = False):
+        """One AdamW step.  ``zero_grad``: also zero the fp32 main grads (on GPUs inside the update
+        kernel, as each element is consumed: no separate fill pass)."""
         from .ops import streams
 
         streams.join()  # weight gradients still on the side stream (ops/streams.py)
@@ -253,7 +255,8 @@ class FusedAdamW:
             C.grad_sumsq_chunks(t.start, t.len, self.grad_buffer, grad_scale, self.norm_buf, t.end)
             C.adamw_step(t.start, t.len, t.wd, None, s.master, s.flat, self.grad_buffer,
                          self.exp_avg, self.exp_avg_sq, self.norm_buf, lr, b1, b2, self.eps,
-                         self.step_count, grad_scale, float(self.grad_clip), t.end, t.mend)
+                         self.step_count, grad_scale, float(self.grad_clip), t.end, t.mend,
+                         s.grad if zero_grad else None)
             return
         # CPU path (plain PyTorch, same math)
         g = self.grad_buffer.float() * grad_scale
@@ -276,6 +279,8 @@ class FusedAdamW:
             denom = (self.exp_avg_sq[sl].sqrt() / math.sqrt(bc2)).add_(self.eps)
             s.master[sl].addcdiv_(self.exp_avg[sl], denom, value=-lr / bc1)
         s.sync_params_from_master()
+        if zero_grad:
+            s.zero_grad()
 
     # ------------------------------------------------------------------ state (by param name)
     def state_dict(self):

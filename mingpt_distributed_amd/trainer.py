@@ -106,7 +106,6 @@ class StepEngine:
         self.measure_comm = False  # hipEvents around dp.finish() (comm_exposed_ms)
         self._comm_events = []
         self._fold_hooks()
-
     def _fold_hooks(self):
         for h in self._hooks:
             h.remove()
@@ -212,8 +211,11 @@ class StepEngine:
 
     def optimizer_step(self):
         with self._range("mingpt::optimizer"):
-            self.opt.step(grad_scale=1.0 / self.world)
-            self.store.zero_grad()
+            if not self.zero1:  # replicated AdamW zeroes the grads inside its update kernel
+                self.opt.step(grad_scale=1.0 / self.world, zero_grad=True)
+            else:
+                self.opt.step(grad_scale=1.0 / self.world)
+                self.store.zero_grad()
         if self.dp is not None:
             order = self.dp.relayout_order()
             if order is not None:

@@ -183,3 +183,12 @@ def test_bucket_plan_tied_embedding_alone():
         wte = st.by_name["transformer.wte.weight"]
         (b,) = [ps for _, _, ps in st.buckets if wte in ps]
         assert b == [wte]
+
+
+def test_fused_adamw_cpu_zero_grad_flag():
+    m = torch.nn.Linear(4, 3)
+    s = FlatParamStore(m)
+    opt = FusedAdamW(s, lr=1e-2)
+    s.grad.normal_()
+    opt.step(zero_grad=True)
+    assert s.grad.abs().max().item() == 0.0
