@@ -1463,14 +1463,16 @@ int pick_config(int M, int N, int K, int layout) {
   // wgrad: W4 (256^2 tiles, one block per CU, split-K over 256 slots) unless T128 (128^2, two
   // blocks per CU, 512 slots) quantises so much better that it pays for its ~15 % lower per-CU
   // rate.  Both sides through the split-K cost model (rounds x (K-tiles per block + overhead)); a
-  // T128 K-tile is a quarter of the work at 2 blocks per CU and 0.85 of W4's rate: 0.59 W4 K-tiles.
-  // bench_wgrad.py (profiles/round3_streamk_wgrad_ab.txt): gpt2-xl at 16k tokens, qkv 294 vs 366 us
-  // and attention projection 110 vs 130 on T128; every GPT-2 (131k tokens) and LM-head shape on W4.
+  // T128 K-tile is a quarter of the work at 2 blocks per CU and ~0.77 of W4's rate since W4's
+  // TN main loop lost its address VALU (round 4): 0.65 W4 K-tiles (was 0.59 at 0.85).
+  // bench_wgrad.py (profiles/round4_wgrad_pick_xl.txt): gpt2-xl at 16k tokens qkv 257 vs 296 us
+  // and attention projection 102 vs 108 on T128, at 32k tokens 493 vs 523 and 168 vs 173 on W4
+  // (xl B = 32 step +0.7 %); every GPT-2 (131k tokens) and LM-head shape on W4.
   const int nkt = cdiv(K, BK);
   long c4 = 0, c1 = 0;
   choose_split((int)t256, 256, nkt, 6, 1, &c4);
   choose_split(cdiv(M, 128) * cdiv(N, 128), 512, nkt, 3, 1, &c1);
-  return c1 * 59 < c4 * 100 ? 1 : 5;
+  return c1 * 65 < c4 * 100 ? 1 : 5;
 }
 
 template <bool AK, bool BKC, int EPI, bool OUTF32>
