@@ -33,7 +33,7 @@
 #include <type_traits>
 
 #ifndef MG_W4_UNROLL
-#define MG_W4_UNROLL 1  // W4 K-loop unrolled over the ring-slot pattern for m/n-contiguous operands
+#define MG_W4_UNROLL 1  // W4 K-loop unrolled over the ring-slot pattern (compile-time slot offsets)
 #endif
 
 using namespace mg;
@@ -1203,7 +1203,9 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
   // m/n-contiguous operands (the data and weight gradients): the ring's slots interleaved inside
   // each 128-column half-image (16 KiB per slot and half), so that with the K-loop unrolled over
   // the slot pattern every transposed read's slot offset is a constant in its offset field
-  constexpr bool UNR = MG_W4_UNROLL && (!AK || !BKC);
+  // (every layout: the all-k-contiguous forward gained +0.4 % of the step too, its slot bases then
+  // fold into the reads' offsets; profiles/round4_w4_nt_unroll_ab.txt)
+  constexpr bool UNR = MG_W4_UNROLL;
   constexpr int AS = AK ? WK::A_SLOT : 16384, AHS = 2 * 16384;  // A: slot / half-image strides
   constexpr int BS = BKC ? WK::B_SLOT : 16384, BHS = 3 * 16384;  // B: 3 slots
   Stager<AK, 256, 4, AHS> sta;
