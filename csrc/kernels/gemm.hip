@@ -32,6 +32,9 @@
 #include "kernels.h"
 #include <type_traits>
 
+#ifndef MG_T128_UNROLL
+#define MG_T128_UNROLL 1  // two-stage block GEMM K-loop unrolled over its stages
+#endif
 #ifndef MG_W4_UNROLL
 #define MG_W4_UNROLL 1  // W4 K-loop unrolled over the ring-slot pattern (compile-time slot offsets)
 #endif
@@ -776,7 +779,53 @@ __global__ __launch_bounds__(CF::NT, 2) void gemm_kernel(const GemmArgs args) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
-  for (int kt = 0; kt < nk; ++kt) {
+  // two stages: the K-loop unrolled by 2 so each stage's base is a constant that goes into the
+  // transposed reads' offset fields (the W4 slot unroll, same reasoning)
+  auto ktile2 = [&](int kt, auto st_c) __attribute__((always_inline)) {
+    constexpr int ST = decltype(st_c)::value;
+    constexpr int OA = ST * CF::STAGE, OB = OA + CF::A_BYTES, ON = (ST ^ 1) * CF::STAGE;
+    const int kn = kt + 1;
+    if (kn < nk) {  // its stage was last read in iteration kt-1: free since that barrier
+      sta.stage(smem + ON, kn);
+      stb.stage(smem + ON + CF::A_BYTES, kn);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[CF::FM], fb[CF::FN];
+#pragma unroll
+      for (int i = 0; i < CF::FM; ++i)
+        fa[i] = ks ? frag_k<AK, 1, 16384, OA>(smem, wm * CF::FM + i, lane)
+                   : frag_k<AK, 0, 16384, OA>(smem, wm * CF::FM + i, lane);
+#pragma unroll
+      for (int j = 0; j < CF::FN; ++j)
+        fb[j] = ks ? frag_k<BKC, 1, 16384, OB>(smem, wn * CF::FN + j, lane)
+                   : frag_k<BKC, 0, 16384, OB>(smem, wn * CF::FN + j, lane);
+      if constexpr (!AK || !BKC) {
+        lds_ready(fa);
+        lds_ready(fb, false);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < CF::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < CF::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  // (stage bases must fit the 16-bit offset field: the 64 KiB two-stage T128 ring)
+  constexpr bool UNR2 = MG_T128_UNROLL && CF::STAGES == 2 && CF::SMEM <= 65536;
+  if constexpr (UNR2) {
+    int kt = 0;
+    for (; kt + 2 <= nk; kt += 2) {
+      ktile2(kt, std::integral_constant<int, 0>{});
+      ktile2(kt + 1, std::integral_constant<int, 1>{});
+    }
+    if (kt < nk) ktile2(kt, std::integral_constant<int, 0>{});
+  }
+  for (int kt = 0; kt < (UNR2 ? 0 : nk); ++kt) {
     const char* sa = smem + (kt % CF::STAGES) * CF::STAGE;
     const char* sb = sa + CF::A_BYTES;
     const int kn = kt + CF::STAGES - 1;  // tile to issue now
