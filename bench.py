@@ -28,9 +28,16 @@ group at N = 1 as a plumbing check of those fields.  ``vs_baseline`` divides by 
 same step at the same per-GPU batch, i.e. the per-GPU speedup over stock
 PyTorch-ROCm (the reference publishes no numbers).
 
+Gradient wire dtype: fp32 by default, the reference DDP's precision
+(``/root/reference/mingpt/trainer.py:71``); ``--reduce-dtype bf16`` is a labelled variant
+(``config.grad_reduce_dtype``).  At N > 1 a compute-only pass follows the checksum: the same
+steps with every gradient collective skipped (``StepEngine.train_step_local``), reported as
+``extra.no_comm`` (null at N = 1 and under ZeRO-1), so a 1 -> N loss splits into exposed
+communication vs compute slowed by the collective kernels sharing the CUs.
+
 Fail-fast for N > 1 (the driver's multi-GPU run must end with a diagnosis, not a bare timeout):
-every rank runs a phase watchdog (:class:`PhaseWatchdog`): init, broadcast, warmup, timed steps,
-checksum, collective timing, barrier.  A phase that lasts more than ``--phase-timeout`` seconds
+every rank runs a phase watchdog (:class:`PhaseWatchdog`): init, broadcast, every warmup and
+timed step (one phase each), checksum, collective timing, barrier.  A phase that lasts more than ``--phase-timeout`` seconds
 (default 150) prints the rank, the phase, how long it has been stuck and the gradient buckets
 whose collective has not completed on the device, then exits the rank with status 4 (the
 launcher then stops the others).  The process group's own timeout (``--pg-timeout``, default
@@ -225,8 +232,12 @@ def main():
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--vocab", type=int, default=50257, help="65 = chargpt's character vocabulary")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
-    ap.add_argument("--reduce-dtype", default="bf16", choices=["fp32", "bf16"],
-                    help="gradient dtype on the wire for N > 1 (bf16: half the xGMI bytes)")
+    ap.add_argument("--reduce-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="gradient dtype on the wire for N > 1: fp32 (default, the reference DDP's "
+                         "precision) or bf16 (half the xGMI bytes; reported as a labelled variant)")
+    ap.add_argument("--no-comm-pass", type=int, default=1,
+                    help="N > 1: after the checksum, time the same steps with every gradient "
+                         "collective skipped (dp.no_sync): extra.no_comm (0: skip)")
     ap.add_argument("--zero1", action="store_true",
                     help="shard the AdamW state over the ranks (reduce-scatter + all-gather)")
     ap.add_argument("--profile", default="", help="write a torch.profiler trace to this dir")
@@ -284,7 +295,7 @@ def main():
     g = torch.Generator(device=eng.device).manual_seed(99 + info.rank)
     step = (lambda x, y: eng.graph_step(x, y)) if a.graph else (lambda x, y: eng.train_step([(x, y)]))
 
-    def timed(batch, steps, warmup, profile="", tag=""):
+    def timed(batch, steps, warmup, profile="", tag="", step_fn=step):
         """W untimed steps, then `steps` timed ones between barrier + device syncs; returns
         (max seconds over ranks, last loss, mean exposed-comm ms or None)."""
         nb = 4
@@ -292,15 +303,15 @@ def main():
         ys = [torch.randint(0, a.vocab, (batch, a.seq), device=eng.device, generator=g) for _ in range(nb)]
         for i in range(warmup):
             wd.phase(f"warmup{tag} step {i}")
-            loss = step(xs[i % nb], ys[i % nb])
+            loss = step_fn(xs[i % nb], ys[i % nb])
             if i == 0:
                 sync()  # the first step (bucket relayout broadcast included) completes here
         wd.phase(f"barrier before timed{tag}")
         D.barrier()
         sync()
-        eng.measure_comm = eng.dp is not None and not a.graph and cuda
+        eng.measure_comm = eng.dp is not None and not a.graph and cuda and step_fn is step
         eng.comm_exposed_ms()  # drop warm-up events
-        wd.phase(f"timed{tag} ({steps} steps + device sync)")
+        wd.phase(f"timed{tag} step 0")
         prof = None
         if profile and info.rank == 0:
             prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
@@ -308,7 +319,10 @@ def main():
             prof.__enter__()
         t0 = time.perf_counter()
         for i in range(steps):
-            loss = step(xs[i % nb], ys[i % nb])
+            if i:  # one phase per step: a long healthy run is never mistaken for a hang
+                wd.phase(f"timed{tag} step {i}")
+            loss = step_fn(xs[i % nb], ys[i % nb])
+        wd.phase(f"timed{tag} device sync")
         sync()
         wd.phase(f"barrier after timed{tag}")
         D.barrier()
@@ -341,9 +355,22 @@ def main():
             "global_batch": a.also_batch * N, "comm_exposed_ms": None if comm2 is None else round(comm2, 3),
             "vs_baseline": round(v2 / (base2 * N), 3) if base2 and a.model == "gpt2" and a.seq == 1024 else None}
     wd.phase("checksum")
+    if eng.zero1 and eng.dp is not None:
+        eng.dp.wait_gathers()  # the last step's parameter all-gathers are still in flight
+    sync()
     identical = _ranks_identical(eng, N)
     wd.phase("collective timing")
     coll = _collective_timing(eng, N)
+    # compute-only pass: the same steps with no gradient collective, so the 1 -> N loss splits
+    # into exposed communication (ms_per_step - no_comm) and compute slowed by sharing the node
+    # (no_comm vs the N = 1 step).  Replicas diverge from here on: it runs after the checksum.
+    extra["no_comm"] = None
+    if N > 1 and a.no_comm_pass and eng.dp is not None and not eng.zero1:
+        local = lambda x, y: eng.train_step_local([(x, y)])  # noqa: E731
+        dt3, _, _ = timed(a.batch, a.steps, min(a.warmup, 2), tag=" no_comm", step_fn=local)
+        extra["no_comm"] = {"value": round(a.batch * a.seq * a.steps * N / dt3, 1),
+                            "ms_per_step": round(dt3 / a.steps * 1e3, 3),
+                            "exposed_comm_ms_per_step": round((dt - dt3) / a.steps * 1e3, 3)}
     wd.phase("report")
     diag = _comm_diag(eng, info, N, comm_ms, cuda)
     diag["ranks_identical"] = identical

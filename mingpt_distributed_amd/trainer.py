@@ -231,6 +231,25 @@ class StepEngine:
         self.optimizer_step()
         return total / n
 
+    def train_step_local(self, batches) -> torch.Tensor:
+        """``train_step`` with every gradient collective skipped: each rank updates its replica
+        from its OWN gradients (diagnostics only -- the replicas diverge).  bench.py times it at
+        N > 1 to split the 1 -> N step-time loss into exposed communication and compute slowed
+        by the node's other ranks.  Replicated DP only (ZeRO-1's update needs the reduce-scatter)."""
+        if self.zero1:
+            raise RuntimeError("train_step_local: ZeRO-1's sharded update needs reduced gradients")
+        n = len(batches)
+        total = None
+        for x, y in batches:
+            l = self.forward_backward(self.to_device(x), self.to_device(y), scale=1.0 / n, sync=False)
+            total = l if total is None else total + l
+        gb, self.opt.grad_buffer = self.opt.grad_buffer, self.store.grad  # the local fp32 grads
+        try:
+            self.optimizer_step()
+        finally:
+            self.opt.grad_buffer = gb
+        return total / n
+
     # ------------------------------------------------------------------ hipGraph step
     def graph_step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         """``train_step([(x, y)])`` as ONE hipGraph replay (single process, GPU).

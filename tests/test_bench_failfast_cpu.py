@@ -37,8 +37,9 @@ def _json_line(out: str) -> dict:
     return json.loads(lines[0])
 
 
-def test_two_ranks_report_identical_replicas_and_collective_times():
-    r, _ = _run(["--gpus", "2", *SMALL])
+@pytest.mark.parametrize("extra_args", [[], ["--zero1"], ["--reduce-dtype", "bf16"]])
+def test_two_ranks_report_identical_replicas_and_collective_times(extra_args):
+    r, _ = _run(["--gpus", "2", *SMALL, *extra_args])
     assert r.returncode == 0, r.stderr[-3000:]
     j = _json_line(r.stdout)
     c = j["comm"]
@@ -46,18 +47,28 @@ def test_two_ranks_report_identical_replicas_and_collective_times():
     assert c["ranks_identical"] is True
     assert len(c["bucket_collective_ms"]) == c["n_buckets"] == len(c["bucket_busbw_gbs"])
     assert all(t > 0 for t in c["bucket_collective_ms"])
+    want = "bf16" if "bf16" in extra_args else "fp32"  # fp32 unless asked: the reference's DDP wire
+    assert j["config"]["grad_reduce_dtype"] == want and c["wire_dtype"] == want
+    nc = j["extra"]["no_comm"]
+    if "--zero1" in extra_args:
+        assert nc is None  # the sharded update needs the reduce-scatter
+    else:
+        assert nc["ms_per_step"] > 0 and nc["value"] > 0
+        assert "exposed_comm_ms_per_step" in nc
 
 
 def test_one_rank_reports_null_multi_rank_fields():
     r, _ = _run(["--gpus", "1", *SMALL])
     assert r.returncode == 0, r.stderr[-3000:]
-    c = _json_line(r.stdout)["comm"]
+    j = _json_line(r.stdout)
+    assert j["extra"]["no_comm"] is None
+    c = j["comm"]
     for k in ("ranks_identical", "bucket_collective_ms", "bucket_busbw_gbs", "collective_total_ms",
               "comm_exposed_ms"):
         assert c[k] is None, (k, c[k])
 
 
-@pytest.mark.parametrize("phase", ["timed (3 steps + device sync)", "broadcast"])
+@pytest.mark.parametrize("phase", ["timed step 1", "broadcast"])
 def test_stalled_rank_fails_fast_naming_the_phase(phase):
     limit = 8
     r, dt = _run(["--gpus", "2", *SMALL, "--phase-timeout", str(limit)],
