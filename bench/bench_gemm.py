@@ -14,7 +14,7 @@ import torch
 from mingpt_distributed_amd.ops import gemm as G
 
 
-VARIANTS = ("auto", "t128", "t256", "t256x128", "pp256", "w4", "w4n192")
+VARIANTS = {"auto": 0, "t128": 1, "w4": 5, "w4n192": 6}  # gemm_set_variant codes
 
 
 def timeit(fn, iters=20, warm=3):
@@ -45,7 +45,7 @@ def main():
 
     def both(fn):  # A/B the tile configs of the hand-written kernel in one process
         out = []
-        for v in range(len(VARIANTS)):
+        for v in VARIANTS.values():
             C.gemm_set_variant(v)
             out.append(timeit(fn))
         C.gemm_set_variant(0)

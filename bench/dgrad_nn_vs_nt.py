@@ -21,7 +21,7 @@ for nm, n_in, n_out in (("proj", D, D), ("fc", D, 4 * D), ("qkv", D, 3 * D), ("f
     aux = r(M, n_in) if nm == "fc2_gelu" else None
     epi = "gelu_bwd" if aux is not None else "none"
     out = {"nt_transpose": round(timeit(lambda: G.gemm_dgrad(dy, w, epi=epi, aux=aux)) * 1e3, 1)}
-    for v, name in ((0, "nn_auto"), (4, "nn_PP"), (5, "nn_W4")):
+    for v, name in ((0, "nn_auto"), (1, "nn_T128"), (5, "nn_W4")):
         C.gemm_set_variant(v)
         out[name] = round(timeit(lambda: G.gemm_nn(dy, w, epi=epi, aux=aux)) * 1e3, 1)
     C.gemm_set_variant(0)

@@ -361,24 +361,23 @@ void bias_grad(const at::Tensor& dy, const at::Tensor& db) {
 void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t layout, int64_t epi,
           const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
           const c10::optional<at::Tensor>& resid, double p, int64_t seed, int64_t M, int64_t N,
-          const c10::optional<at::Tensor>& dbias, const c10::optional<at::Tensor>& delta,
-          int64_t dT, int64_t dH, int64_t dhd, int64_t row0) {
+          const c10::optional<at::Tensor>& dbias) {
   CHECK_BF16(a); CHECK_BF16(b); CHECK_DEV(c);
   CHECK_CONTIG(a); CHECK_CONTIG(b); CHECK_CONTIG(c);
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm: 2-D operands required");
-  TORCH_CHECK(layout >= 0 && layout <= 2 && epi >= 0 && epi <= 5, "gemm: bad layout/epilogue");
+  TORCH_CHECK(layout >= 0 && layout <= 2 && epi >= 0 && epi <= 4, "gemm: bad layout/epilogue");
   const int64_t lda = a.size(1), ldb = b.size(1), ldc = c.size(1);
   TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0, "gemm: row strides must be multiples of 8");
   TORCH_CHECK(M > 0 && N > 0 && M <= c.size(0) && N <= ldc, "gemm: output bounds");
   int64_t K, a_ext, b_ext, ka, kb;
   if (layout == 0) {
     K = lda; ka = lda; kb = ldb; a_ext = a.size(0); b_ext = b.size(0);
-    TORCH_CHECK(lda == ldb && epi != 5, "gemm NT: K mismatch");
+    TORCH_CHECK(lda == ldb, "gemm NT: K mismatch");
     TORCH_CHECK(M <= a_ext && N <= (epi == 0 ? ldc : b_ext), "gemm NT: shape mismatch");
     TORCH_CHECK(c.scalar_type() == at::kBFloat16, "gemm NT: bf16 output");
   } else if (layout == 1) {
     K = lda; ka = lda; kb = b.size(0); a_ext = a.size(0); b_ext = ldb;
-    TORCH_CHECK(kb <= K && M <= a_ext && N <= ldb && (epi == 0 || epi == 4 || epi == 5), "gemm NN: shape mismatch");
+    TORCH_CHECK(kb <= K && M <= a_ext && N <= ldb && (epi == 0 || epi == 4), "gemm NN: shape mismatch");
     TORCH_CHECK(c.scalar_type() == at::kBFloat16, "gemm NN: bf16 output");
   } else {
     K = a.size(0); ka = K; kb = b.size(0); a_ext = lda; b_ext = ldb;
@@ -393,7 +392,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     bias_p = bp(*bias);
   }
   bf16_t* aux_p = nullptr;
-  if (epi == 2 || epi == 4 || epi == 5) {
+  if (epi == 2 || epi == 4) {
     TORCH_CHECK(aux.has_value() && aux->defined(), "gemm: epilogue needs aux");
     CHECK_BF16(*aux); CHECK_CONTIG(*aux);
     TORCH_CHECK(aux->numel() == c.numel(), "gemm: aux shape");
@@ -414,22 +413,10 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     TORCH_CHECK(epi == 4 && dbias->numel() >= N, "gemm: dbias only with the gelu_bwd epilogue");
     dbias_p = fp(*dbias);
   }
-  mg::GemmDelta dl{nullptr, 1, 1, 8, 0};
-  if (epi == 5) {
-    // attention delta fused into the dO data gradient: one 8-lane group per (row, head) inside the
-    // wave-tile rows (every NN tile config is >= 64 columns per wave: hd must divide 64)
-    TORCH_CHECK(delta.has_value() && delta->defined(), "gemm: epilogue 5 needs delta");
-    CHECK_F32(*delta); CHECK_CONTIG(*delta);
-    TORCH_CHECK((dhd == 8 || dhd == 16 || dhd == 32 || dhd == 64) && N == dH * dhd && ldc == N && dT > 0 &&
-                    row0 >= 0,
-                "gemm: delta epilogue shape (hd in {8,16,32,64}, N = H hd, whole sequences)");
-    TORCH_CHECK(delta->numel() >= (row0 + M) * dH, "gemm: delta too short");
-    dl = mg::GemmDelta{fp(*delta), (int)dT, (int)dH, (int)dhd, (long)row0};
-  }
   DevGuard g(a.device());
   mg::gemm((int)layout, (int)epi, bp(a), bp(b), c.data_ptr(), lda, ldb, ldc, (int)M, (int)N, (int)K,
            (int)a_ext, (int)b_ext, (int)ka, (int)kb, bias_p, aux_p, res_p, (float)p, (uint64_t)seed,
-           cur_stream(), (size_t)a.numel() * 2, (size_t)b.numel() * 2, dbias_p, epi == 5 ? &dl : nullptr);
+           cur_stream(), (size_t)a.numel() * 2, (size_t)b.numel() * 2, dbias_p);
 }
 
 // ------------------------------------------------------------------------------- attention
@@ -453,8 +440,7 @@ std::vector<at::Tensor> attention_fwd(const at::Tensor& qkv, int64_t B, int64_t 
 
 at::Tensor attention_bwd(const at::Tensor& qkv, const at::Tensor& out, const at::Tensor& dout,
                          const at::Tensor& lse, const at::Tensor& mask, int64_t B, int64_t T,
-                         int64_t H, double p, int64_t seed, const c10::optional<at::Tensor>& dbias,
-                         const c10::optional<at::Tensor>& delta_in) {
+                         int64_t H, double p, int64_t seed, const c10::optional<at::Tensor>& dbias) {
   CHECK_BF16(qkv); CHECK_BF16(out); CHECK_BF16(dout); CHECK_F32(lse);
   CHECK_CONTIG(qkv); CHECK_CONTIG(out); CHECK_CONTIG(dout);
   const int64_t D3 = qkv.size(-1), D = D3 / 3, hd = D / H;
@@ -464,13 +450,7 @@ at::Tensor attention_bwd(const at::Tensor& qkv, const at::Tensor& out, const at:
   DevGuard g(qkv.device());
   auto dqkv = at::empty_like(qkv);
   auto opts = qkv.options().dtype(at::kFloat);
-  // delta = rowsum(dO * O) per (b, h, t): computed here, or handed in (the dO GEMM's epilogue 5)
-  const bool have_delta = delta_in.has_value() && delta_in->defined();
-  if (have_delta) {
-    CHECK_F32(*delta_in); CHECK_CONTIG(*delta_in);
-    TORCH_CHECK(delta_in->numel() == B * H * T, "attention_bwd: delta must be fp32 [B*H*T]");
-  }
-  auto delta = have_delta ? *delta_in : at::empty({B * H * T}, opts);
+  auto delta = at::empty({B * H * T}, opts);  // rowsum(dO * O) per (b, h, t), attn_bwd_pre_kernel
   // fp32 dQ accumulator (persistent mode) or per-key-block partials (attention_train.hip)
   auto dq = at::empty({(int64_t)mg::attention_bwd_workspace_floats((int)B, (int)T, (int)H, (int)hd)}, opts);
   const uint32_t* mp = nullptr;
@@ -488,7 +468,7 @@ at::Tensor attention_bwd(const at::Tensor& qkv, const at::Tensor& out, const at:
     db = fp(*dbias);
   }
   mg::attention_bwd(bp(qkv), bp(out), bp(dout), fp(lse), mp, fp(delta), fp(dq), bp(dqkv), (int)B,
-                    (int)T, (int)H, (int)hd, (float)p, (uint64_t)seed, cur_stream(), db, have_delta);
+                    (int)T, (int)H, (int)hd, (float)p, (uint64_t)seed, cur_stream(), db);
   return dqkv;
 }
 
@@ -688,15 +668,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dropout_bias_grad", &dropout_bias_grad);
   m.def("gemm", &gemm, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("layout"), py::arg("epi"),
         py::arg("bias"), py::arg("aux"), py::arg("resid"), py::arg("p"), py::arg("seed"), py::arg("M"),
-        py::arg("N"), py::arg("dbias") = py::none(), py::arg("delta") = py::none(), py::arg("dT") = 1,
-        py::arg("dH") = 1, py::arg("dhd") = 8, py::arg("row0") = 0);
+        py::arg("N"), py::arg("dbias") = py::none());
   m.def("gemm_set_variant", &mg::gemm_set_variant);
   m.def("gemm_get_variant", &mg::gemm_get_variant);
   m.def("attention_set_bwd_mode", &mg::attention_set_bwd_mode);
   m.def("attention_fwd", &attention_fwd);
   m.def("attention_bwd", &attention_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"),
         py::arg("mask"), py::arg("B"), py::arg("T"), py::arg("H"), py::arg("p"), py::arg("seed"),
-        py::arg("dbias") = py::none(), py::arg("delta") = py::none());
+        py::arg("dbias") = py::none());
   m.def("gemv", &gemv, py::arg("x"), py::arg("W"), py::arg("epi"), py::arg("bias") = py::none(),
         py::arg("resid") = py::none(), py::arg("ldy") = 0, py::arg("lnw") = py::none(),
         py::arg("lnb") = py::none(), py::arg("eps") = 1e-5, py::arg("am_part") = py::none(),

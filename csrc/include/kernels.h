@@ -85,21 +85,13 @@ void dropout_bias_grad(const bf16_t* dy, bf16_t* dx, float* db, long M, int N, f
                        hipStream_t stream);
 
 // gemm.hip -- layout 0 NT (fwd), 1 NN (dgrad), 2 TN (wgrad, fp32 accumulate)
-// epi: 0 none, 1 bias, 2 bias+gelu (pre -> aux), 3 resid + dropout(acc + bias), 4 acc*gelu'(aux)
-// EPI 5 (NN data gradient of the attention projection, dO = dZ Wo): the attention backward's
-// delta[(b H + h) T + t] = sum_d dO[m, h hd + d] * O[m, h hd + d] (O = aux), m = row0 + row
-struct GemmDelta {
-  float* delta;
-  int T, H, hd;  // hd in {8, 16, 32, 64}
-  long row0;
-};
+// epi: 0 none, 1 bias, 2 bias+gelu (gelu'(z) -> aux), 3 resid + dropout(acc + bias), 4 acc*gelu'(aux)
 void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long lda, long ldb,
           long ldc, int M, int N, int K, int a_ext, int b_ext, int ka, int kb, const bf16_t* bias,
           bf16_t* aux, const bf16_t* resid, float p, uint64_t seed, hipStream_t stream,
           size_t a_bytes, size_t b_bytes,  // operand sizes in bytes (< 4 GiB for the DMA path)
-          float* dbias = nullptr,          // EPI 4 only: += column sums of C (bias gradient)
-          const GemmDelta* dl = nullptr);  // EPI 5 only
-void gemm_set_variant(int v);  // tile config override: 0 auto (per shape), 1..5 forced (gemm.hip)
+          float* dbias = nullptr);         // EPI 4 only: += column sums of C (bias gradient)
+void gemm_set_variant(int v);  // tile config override: 0 auto (per shape), 1 T128, 5 W4, 6 W4-192
 void gemm_set_debug_buffer(unsigned long long* p);  // MG_GEMM_STAMPS diagnostic builds
 int gemm_get_variant();
 
@@ -121,8 +113,7 @@ void attention_set_bwd_mode(int mode);  // 0 auto, 1 persistent (b, h) workgroup
 // backward kernels where the schedule allows
 void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse,
                    const uint32_t* dmask, float* delta, float* dq, bf16_t* dqkv, int B, int T, int H,
-                   int hd, float p, uint64_t seed, hipStream_t stream, float* dbias = nullptr,
-                   bool delta_ready = false);  // delta already holds rowsum(dO * O) (gemm EPI 5)
+                   int hd, float p, uint64_t seed, hipStream_t stream, float* dbias = nullptr);
 
 // one decode step: appends K/V of qkv_new [B, 3D] at row pos of cache [B, Tmax, 3D]; out [B, D].
 // part (attention_decode_part_floats(B, H, hd) floats) and counters (B * H, zero; the kernel leaves

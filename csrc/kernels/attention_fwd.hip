@@ -422,9 +422,8 @@ MG_DEVICE uint32_t pair_mask(uint32_t kw, int j) {
 //  * the causal mask touches only each wave's last (diagonal) tile.
 //  * the workgroups of one (b, h) run 8 apart in the grid (one XCD under round-robin placement:
 //    K / V shared through that XCD's L2), heaviest query block first within the group.
-// Timing-only ablation builds (MG_EXTRA_FLAGS=-DMG_ABL_<X>, outputs wrong on purpose; PERF.md round
-// 4): NODROP (P not masked), NOEXP (no exp2), NOBAR (no per-tile barrier), NOLOAD (no K / V
-// staging), NOPV (no PV MFMAs).
+// (The round-4 timing-only ablations of this kernel -- outputs wrong on purpose -- live outside the
+// production source: bench/dev/attn_ablations.patch, applied to a scratch copy by scripts/build_variant.sh.)
 template <int NKS, bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a) {
   static_assert(NKS >= 1 && NKS <= 4, "pipelined forward: head dim <= 64");
@@ -569,11 +568,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
       uint32_t u[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-#ifdef MG_ABL_NOEXP
-        const float p0 = c[8 * st + 2 * i], p1 = c[8 * st + 2 * i + 1];
-#else
         const float p0 = fexp2(c[8 * st + 2 * i]), p1 = fexp2(c[8 * st + 2 * i + 1]);
-#endif
         if (!LM) rs += p0 + p1;
         u[i] = pack2(p0, p1);
       }
@@ -581,9 +576,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
     };
     // dropped P: pair j's mask = sign-extended bits j / 16 + j of the row word
     auto dropped = [&](const bf16x8& pu, int j, uint32_t kw) __attribute__((always_inline)) -> bf16x8 {
-#ifdef MG_ABL_NODROP
-      return pu;
-#endif
       if constexpr (!DROP) return pu;
       const uint4 u = __builtin_bit_cast(uint4, pu);
       return __builtin_bit_cast(bf16x8, make_uint4(u.x & pair_mask(kw, j), u.y & pair_mask(kw, j + 1),
@@ -643,10 +635,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
               (n & 1) ? lds_tr_at(sv + rb, ta1, tb1) : lds_tr_at(sv + rb, ta0, tb0), pd, o[n], 0, 0, 0);
         if (LM) lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pu, lacc, 0, 0, 0);
       };
-#ifdef MG_ABL_NOPV
-      lacc[0] += __builtin_bit_cast(float, __builtin_bit_cast(uint4, pd00).x ^ __builtin_bit_cast(uint4, pd01).y ^ __builtin_bit_cast(uint4, pd10).z ^ __builtin_bit_cast(uint4, pd11).w);
-      return;
-#endif
       pv(pd00, pu00, 0);  // 16-row aligned LDS row bases: immediates
       pv(pd01, pu01, 16 * ROWB);
       pv(pd10, pu10, 32 * ROWB);
@@ -669,18 +657,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(const AttnArgs a)
     const int nt = bi ? ntB : ntA;
     auto stage = [&](int t, auto&& body) __attribute__((always_inline)) {
       const int u = u0 + t;
-#ifndef MG_ABL_NOLOAD
       store_tile(sK + (u & 1) * TILE, rk);
       store_tile(sV + ((u + 1) & 1) * TILE, rv);
       load_k(rk, min(u + 3, nall - 1));
       load_v(rv, min(u + 2, nall - 1));
-#endif
       const uint32_t kw_next = DROP ? row_word(min(t + 1, max(tw, 0))) : 0u;
       body();
       kw_cur = kw_next;
-#ifndef MG_ABL_NOBAR
       __syncthreads();
-#endif
     };
     // Per wave: steady tiles t < tw, the diagonal tile tw, then idle tiles up to the workgroup's
     // nt.  The trip counts differ between waves but every iteration has exactly one barrier, so

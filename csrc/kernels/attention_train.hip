@@ -185,9 +185,8 @@ MG_DEVICE void tr_reduce32(float (&v)[NV], int lane) {
 //  * attention dropout: the forward's keep bits (attn_dropmask_kernel), one word per query and
 //    32-key half tile, staged BQ queries x KW words per tile.
 //  * BQ = 128 queries per tile (key-block mode, hd <= 64): the dS^T image is two 64-query halves.
-// Timing-only ablation builds (MG_EXTRA_FLAGS=-DMG_ABL_BWD_<X>, outputs wrong on purpose; PERF.md
-// round 4): NOSM (no softmax-gradient VALU), NOKV (no dV / dK MFMAs), NOSTAGE (no next-tile
-// loads), NODQST (no dQ stores).
+// (The round-4 timing-only ablations of this kernel -- outputs wrong on purpose -- live outside the
+// production source: bench/dev/attn_ablations.patch, applied to a scratch copy by scripts/build_variant.sh.)
 template <int NKS, int KW, bool PERSIST>
 __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) {
   constexpr int BQ = bwd_bq<NKS, PERSIST>();
@@ -345,9 +344,7 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
       // one to reach the tile writes bf16
       const int last_kb = min(nkb - 1, (qbase + BQ - 1) / KB);
       const bool first = part || kb == 0, last = !part && kb == last_kb;
-#ifndef MG_ABL_BWD_NOSTAGE
       if (more) issue(qt + 1);
-#endif
       // previous key blocks' dQ sums of this wave's tiles: LDS-DMA'd now (no registers held),
       // added after the dQ MFMAs (a load in the store loop exposed a memory latency per tile)
       float* pvs = reinterpret_cast<float*>(smem + OFF_PV) + (my_split == 0 ? w : 0) * NTW * 16 * 64;
@@ -412,25 +409,15 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
                                                        0, 0, 0);
         }
         // wave-uniform: only diagonal / past-T tiles pay for the causal mask
-#ifdef MG_ABL_BWD_NOSM
-        if (false)
-#else
         if (wave_kmin + 31 > qsub0 || qsub0 + 31 >= a.T)
-#endif
           bwd_softmax_grad<true>(sacc, dp, dl, mwr, a.T, mykey, mw_bit, qsub0 + 4 * h32);
-#ifndef MG_ABL_BWD_NOSM
         else
           bwd_softmax_grad<false>(sacc, dp, dl, mwr, a.T, mykey, mw_bit, qsub0 + 4 * h32);
-#endif
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
           const bf16x8 pf = pack_frag(sacc, st);
           const bf16x8 dsf = pack_frag(dp, st);
           const int rb = (qs * 32 + 16 * st) * ROWB;  // 16-row aligned: an immediate
-#ifdef MG_ABL_BWD_NOKV
-          dv[0][st] += __builtin_bit_cast(float, __builtin_bit_cast(uint4, pf).x ^ __builtin_bit_cast(uint4, dsf).y);
-          continue;
-#endif
 #pragma unroll
           for (int n = 0; n < NO; ++n) {
             const int hb = (n >> 1) * HQ + rb;
@@ -497,9 +484,6 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
           }
         }
         const int d = n * 32 + l32;
-#ifdef MG_ABL_BWD_NODQST
-        if (dq[0] == 12345.f)
-#endif
         if (part && my_split == 0 && d < a.hd && qbase + qs * 32 + 31 >= kb0) {
           // key-block partial: buffer stores through one descriptor per query tile whose extent
           // ends at row T of this sequence (rows past it are dropped: no per-row branches), row
@@ -697,7 +681,7 @@ namespace mg {
 
 void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse,
                    const uint32_t* dmask, float* delta, float* dq, bf16_t* dqkv, int B, int T, int H,
-                   int hd, float p, uint64_t seed, hipStream_t stream, float* dbias, bool delta_ready) {
+                   int hd, float p, uint64_t seed, hipStream_t stream, float* dbias) {
   (void)seed;
   AttnArgs a{};
   a.B = B; a.T = T; a.H = H; a.hd = hd; a.D = H * hd;
@@ -718,8 +702,7 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
   int lg = 0;
   while ((8 << lg) < hd) ++lg;
   const long nthreads = (long)B * T * H << lg;
-  if (!delta_ready)
-    attn_bwd_pre_kernel<<<(unsigned)cdiv(nthreads, 256), 256, 0, stream>>>(dout, out, delta, B * T, T, H, hd, lg);
+  attn_bwd_pre_kernel<<<(unsigned)cdiv(nthreads, 256), 256, 0, stream>>>(dout, out, delta, B * T, T, H, hd, lg);
   switch (nks_for(hd)) {
     case 1: launch_bwd<1, 8>(a, stream); break;
     case 2: launch_bwd<2, 8>(a, stream); break;

@@ -10,10 +10,13 @@
 //   layout TN: A' = A[K,M]^T (m contiguous), B' = B[K,N] (n contiguous)  -> wgrad   dW += dy^T x
 //
 // Design (see /opt/skills/guides/cdna_hip_programming.md §5):
-//  * v_mfma_f32_16x16x32_bf16, BK = 64, tile configs chosen per shape:
-//      T128: 128x128 tile, 4 waves (2x2) of 64x64, 64 KiB LDS -> 2 workgroups / CU
-//      T256: 256x256 tile, 8 waves (2x4) of 128x64, 128 KiB LDS -> 1 workgroup / CU (2 waves/SIMD)
-//      T2x1: 256x128 tile, 8 waves (4x2) of 64x64, 96 KiB LDS
+//  * v_mfma_f32_16x16x32_bf16, BK = 64, tile configs chosen per shape (pick_config):
+//      W4:   256x256 (or 256x192) tile, 4 waves (2x2) of 128x128 (128x96), 160 KiB LDS, one wave
+//            per SIMD holding the whole register file (the default for every large shape)
+//      T128: 128x128 tile, 4 waves (2x2) of 64x64, 64 KiB LDS -> 2 workgroups / CU (small outputs,
+//            and weight gradients whose tile count quantises badly onto 256 CUs at 256^2)
+//    (the 8-wave 256x256 ping-pong, 256x256 / 8-wave and 256x128 block configs of rounds 1-2 never
+//    won a shape once W4 existed and were deleted in round 5; PERF.md)
 //  * LDS-DMA staging (buffer_load_dwordx4 ... lds): global -> LDS without VGPRs, tile k+1 in flight
 //    while tile k is multiplied (2-stage ring, one vmcnt(0) + barrier per K-step).  The buffer range
 //    check zero-fills every row / column / K tail, so no tail code runs in the main loop.
@@ -24,20 +27,14 @@
 //  * operands swapped in the MFMA (C^T = B'^T A'^T): each lane holds 4 consecutive n of one row m,
 //    so epilogue stores are 8 B (bf16) / 16 B (fp32).
 //  * XCD-aware bijective block remap + GROUP_M ordering (blocks sharing A rows share an XCD's L2).
-//  * epilogues: none | +bias | +bias,GELU (pre-activation also stored) |
-//    resid + dropout(acc + bias) (Philox mask, same element mapping as elementwise.hip) |
-//    acc * aux (GELU' from the forward) | fp32 accumulate (the main-grad buffer), split-K via
-//    LDS-staged atomics.
+//  * epilogues: none | +bias | +bias,GELU (GELU'(z) also stored) |
+//    resid + dropout(acc + bias) (counter-hash row-block mask, common.h) |
+//    acc * aux (GELU' from the forward, + the fc bias gradient's column sums) | fp32 accumulate
+//    (the main-grad buffer), split-K via LDS-staged atomics.
 #include "common.h"
 #include "kernels.h"
 #include <type_traits>
 
-#ifndef MG_T128_UNROLL
-#define MG_T128_UNROLL 1  // two-stage block GEMM K-loop unrolled over its stages
-#endif
-#ifndef MG_W4_UNROLL
-#define MG_W4_UNROLL 1  // W4 K-loop unrolled over the ring-slot pattern (compile-time slot offsets)
-#endif
 
 using namespace mg;
 
@@ -63,12 +60,8 @@ struct Cfg {
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   static constexpr int STAGE = A_BYTES + B_BYTES;
   static constexpr int SMEM = STAGES * STAGE;
-  // LDS-DMA wave-instructions one wave issues per K-step (for the counted vmcnt)
-  static constexpr int DMA_PER_STEP = BM / 8 / NW + BN / 8 / NW;
 };
 using T128 = Cfg<128, 128, 2, 2>;
-using T256 = Cfg<256, 256, 2, 4>;
-using T2x1 = Cfg<256, 128, 4, 2, 3>;  // 3-stage ring: two K-steps in flight, 144 KiB
 
 struct GemmArgs {
   const bf16_t* A;
@@ -91,14 +84,11 @@ struct GemmArgs {
   uint64_t a_bytes, b_bytes;  // operand sizes; each block's descriptor spans <= 4 GiB from its origin
   unsigned long long* dbg;    // MG_GEMM_STAMPS diagnostic builds only: per-wave phase timestamps
   float* dbias;               // EPI 4: += column sums of the output (the bias gradient), or null
-  float* delta;               // EPI 5: attention delta[(b H + h) T + t] = sum_d C[m, h hd + d] aux[m, ..]
-  int dT, dH, dhd;            // EPI 5: sequence length, heads, head dim (hd in {8, 16, 32, 64})
-  long drow0;                 // EPI 5: global row of this launch's row 0 (row-chunked launches)
   int nt_out;                 // non-temporal bf16 output stores (see gemm() below)
 };
 
 static unsigned long long* g_dbg = nullptr;  // MG_GEMM_STAMPS builds: stamp buffer
-static int g_variant = 0;  // 0 auto, 1 force T128, 2 force T256, 3 force T2x1, 4 force PP, 5 force W4, 6 force W4 BN=192
+static int g_variant = 0;  // 0 auto, 1 force T128, 5 force W4, 6 force W4 BN=192 (2-4: deleted configs)
 
 // Chunk swizzle of the m/n-contiguous [64 k][256 B] half-images: rows 8 g + q (q < 4) of one
 // transposed read get 8 distinct chunk pairs (conflict-free ds_read_b64_tr_b16), and bit 2 of the
@@ -414,25 +404,12 @@ MG_DEVICE void staged_rows(const GemmArgs& args, const char* st, const uint4 (&s
       const float4 b = *reinterpret_cast<const float4*>(row + p * 32 + 16);
       float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
       const uint32_t w[4] = {sd[it].x, sd[it].y, sd[it].z, sd[it].w};
-      float dot = 0.f;  // EPI 5: this piece's share of sum_d dO * O
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float s = bf2f((w[k >> 1] >> (16 * (k & 1))) & 0xffffu);
-        if constexpr (EPI == 5) dot = __builtin_fmaf(v[k], s, dot);
-        else v[k] = EPI == 3 ? v[k] + s : v[k] * s;
+        v[k] = EPI == 3 ? v[k] + s : v[k] * s;
       }
       y = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
-      if constexpr (EPI == 5) {
-        // the hd / 8 consecutive lanes of a (row, head) -- aligned inside the row's PR lanes,
-        // since the wave-tile width is a multiple of hd -- fold, the first one stores
-        const int g8 = args.dhd >> 3;
-        for (int o = 1; o < g8; o <<= 1) dot += __shfl_xor(dot, o, 64);
-        if ((p & (g8 - 1)) == 0 && (!CHECK || m < args.M)) {
-          const long gm = args.drow0 + m;
-          const int bb = (int)(gm / args.dT), t = (int)(gm % args.dT);
-          args.delta[((long)bb * args.dH + n / args.dhd) * args.dT + t] = dot;
-        }
-      }
       if constexpr (EPI == 4 && staged_dbias<CF>()) {  // column sums (fp32, before the bf16 rounding)
         if constexpr (CHECK) {
           const bool ok = m < args.M;
@@ -473,7 +450,7 @@ template <class CF, int EPI, int LDSW>
 MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int m0, int n0,
                                int wm, int wn, int wid, int lane, char* smem,
                                unsigned long long* est = nullptr) {
-  constexpr bool F32 = EPI == 3 || EPI == 4 || EPI == 5;  // staged before a bf16 side input is applied
+  constexpr bool F32 = EPI == 3 || EPI == 4;  // staged before a bf16 side input is applied
   constexpr int PL = EPI == 2 ? 2 : 1;           // planes: y (+ GELU' for EPI 2)
   constexpr int S = CF::WTN * (F32 ? 4 : 2) + 16;  // row stride: rows 4 banks apart (b64/b128 writes)
   constexpr int CHF = stage_chf(CF::FM, 16 * S * PL, LDSW);  // fragment rows per pass
@@ -763,24 +740,18 @@ __global__ __launch_bounds__(CF::NT, 2) void gemm_kernel(const GemmArgs args) {
   Stager<BKC, CF::BN, CF::NW> stb;
   sta.init(args.A, args.a_bytes, args.lda, m0, args.a_ext, kbeg, args.ka, kbeg + args.kchunk, wid, lane);
   stb.init(args.B, args.b_bytes, args.ldb, n0, args.b_ext, kbeg, args.kb, kbeg + args.kchunk, wid, lane);
-  // prologue: STAGES-1 tiles in flight
-#pragma unroll
-  for (int st = 0; st < CF::STAGES - 1; ++st) {
-    if (st < nk) {
-      char* dst = smem + st * CF::STAGE;
-      sta.stage(dst, st);
-      stb.stage(dst + CF::A_BYTES, st);
-    }
+  static_assert(CF::STAGES == 2 && CF::SMEM <= 65536, "two-stage ring with 16-bit stage offsets");
+  // prologue: tile 0 in flight
+  if (nk > 0) {
+    sta.stage(smem, 0);
+    stb.stage(smem + CF::A_BYTES, 0);
   }
-  if constexpr (CF::STAGES == 3) {
-    if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CF::DMA_PER_STEP) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   // two stages: the K-loop unrolled by 2 so each stage's base is a constant that goes into the
-  // transposed reads' offset fields (the W4 slot unroll, same reasoning)
+  // transposed reads' offset fields (the W4 slot unroll, same reasoning); per K-tile: DMA of tile
+  // kt+1 into the other stage, the two k32 steps, then tile kt+1 landed (this wave's DMA) and every
+  // wave's LDS reads of stage kt retired before the barrier
   auto ktile2 = [&](int kt, auto st_c) __attribute__((always_inline)) {
     constexpr int ST = decltype(st_c)::value;
     constexpr int OA = ST * CF::STAGE, OB = OA + CF::A_BYTES, ON = (ST ^ 1) * CF::STAGE;
@@ -815,286 +786,14 @@ __global__ __launch_bounds__(CF::NT, 2) void gemm_kernel(const GemmArgs args) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };
-  // (stage bases must fit the 16-bit offset field: the 64 KiB two-stage T128 ring)
-  constexpr bool UNR2 = MG_T128_UNROLL && CF::STAGES == 2 && CF::SMEM <= 65536;
-  if constexpr (UNR2) {
-    int kt = 0;
-    for (; kt + 2 <= nk; kt += 2) {
-      ktile2(kt, std::integral_constant<int, 0>{});
-      ktile2(kt + 1, std::integral_constant<int, 1>{});
-    }
-    if (kt < nk) ktile2(kt, std::integral_constant<int, 0>{});
+  int kt = 0;
+  for (; kt + 2 <= nk; kt += 2) {
+    ktile2(kt, std::integral_constant<int, 0>{});
+    ktile2(kt + 1, std::integral_constant<int, 1>{});
   }
-  for (int kt = 0; kt < (UNR2 ? 0 : nk); ++kt) {
-    const char* sa = smem + (kt % CF::STAGES) * CF::STAGE;
-    const char* sb = sa + CF::A_BYTES;
-    const int kn = kt + CF::STAGES - 1;  // tile to issue now
-    if (kn < nk) {  // its stage was last read in iteration kt-1: free since that barrier
-      char* dst = smem + (kn % CF::STAGES) * CF::STAGE;
-      sta.stage(dst, kn);
-      stb.stage(dst + CF::A_BYTES, kn);
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 fa[CF::FM], fb[CF::FN];
-      // k-step as a template constant (frag_k: offset-field transposed reads)
-#pragma unroll
-      for (int i = 0; i < CF::FM; ++i)
-        fa[i] = ks ? frag_k<AK, 1>(sa, wm * CF::FM + i, lane) : frag_k<AK, 0>(sa, wm * CF::FM + i, lane);
-#pragma unroll
-      for (int j = 0; j < CF::FN; ++j)
-        fb[j] = ks ? frag_k<BKC, 1>(sb, wn * CF::FN + j, lane) : frag_k<BKC, 0>(sb, wn * CF::FN + j, lane);
-      if constexpr (!AK || !BKC) {
-        lds_ready(fa);
-        lds_ready(fb, false);
-      }
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < CF::FM; ++i)
-#pragma unroll
-        for (int j = 0; j < CF::FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    // tile kt+1 must have landed (this wave's DMA), every wave's LDS reads of stage kt retired;
-    // with 3 stages the DMA of tile kt+2 stays in flight across the barrier (counted vmcnt).
-    if constexpr (CF::STAGES == 3) {
-      if (kn < nk) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(CF::DMA_PER_STEP) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-  }
+  if (kt < nk) ktile2(kt, std::integral_constant<int, 0>{});
 
   epilogue<CF, EPI, OUTF32, CF::SMEM / CF::NW>(args, acc, m0, n0, wm, wn, wid, lane, smem);
-}
-
-// ============================================================================================
-// Ping-pong 256x256 kernel ("PP"): the deep-pipelined structure for large tiles.
-//
-// 8 waves (2 x 4), wave tile 128 x 64, BK = 64.  A K-tile is consumed in 4 phases (k-half ks,
-// row-half ih of the wave tile); each phase = {ds_read its fragments, issue 2 LDS-DMA rounds,
-// [counted vmcnt], s_barrier, lgkmcnt(0), 16 MFMAs, s_barrier}.  Wave group wr = 1 runs one
-// barrier behind group 0, so on every SIMD (waves w and w+4 share one) one wave multiplies while
-// the other reads LDS and issues DMA.
-//
-// LDS: 2 K-tile buffers x (A 32 KiB + B 32 KiB) + 16 KiB sink.  An operand image is split in
-// 4 "rounds" of 8 KiB = (half h of the 256 rows/cols, k-half kh); one round = one 1-KiB
-// buffer_load...lds per wave.  k-contiguous operands use [kh][256 rows][64 B] images (chunk ^
-// ((row >> 1) & 3): conflict-free ds_read_b128), m/n-contiguous operands the [h][64 k][256 B]
-// half-images of the T128/T256 kernels (ds_read_b64_tr_b16).
-//
-// Schedule in window W (tile W's 4 phases, buffer W & 1):
-//   p0: K0 rounds of B (tile W+1)   p1: K1 rounds of A (W+1)   p2: K1 rounds of B (W+1)
-//   p3: K0 rounds of A (W+2)        vmcnt(6) at p1 (retires K1 of W) and p3 (K0 of W+1)
-// A round is restaged >= 2 phases after its last read (the stagger lets the partner group's reads
-// of the previous phase still be in flight one phase later), and read one phase after the wait that
-// retired it.  Rounds past the last K-tile go to the sink with an out-of-range offset, so every
-// phase issues exactly 2 DMA instructions and the counted waits stay exact in the tail.
-namespace ppk {
-constexpr int BUF = 65536;
-constexpr int SINK = 2 * BUF;
-constexpr int SMEM = 2 * BUF + 16384;
-
-template <bool KC>
-MG_DEVICE int round_off(int h, int kh) { return KC ? kh * 16384 + h * 8192 : h * 16384 + kh * 8192; }
-
-template <bool KC>
-MG_DEVICE bf16x8 frag(const char* img, int sb, int ks, int lane) {
-  if constexpr (KC) {
-    const int row = sb * 16 + (lane & 15), ch = lane >> 4;
-    return *reinterpret_cast<const bf16x8*>(img + ks * 16384 + row * 64 + ((ch ^ ((row >> 1) & 3)) << 4));
-  } else {
-    return ::frag<false>(img, sb, ks, lane);
-  }
-}
-
-// Per-wave DMA piece of round (h, kh) of one operand: byte offset at K-tile 0 relative to the
-// split's K start (kOOB when its row/col is out of range), and its k position for the per-lane
-// check of a partial last K-tile.
-struct Piece {
-  uint32_t off0;
-  int kpos;
-};
-
-template <bool KC>
-MG_DEVICE Piece make_piece(long ld, int r0, int ext, int h, int kh, int wid, int lane) {
-  Piece p;
-  if constexpr (KC) {
-    const int row = h * 128 + wid * 16 + (lane >> 2);
-    const int ch = (lane & 3) ^ ((row >> 1) & 3);
-    const int gr = r0 + row;
-    p.kpos = kh * 32 + ch * 8;
-    p.off0 = gr < ext ? (uint32_t)(((long)gr * ld + p.kpos) * 2) : kOOB;
-  } else {
-    const int krow = kh * 32 + wid * 4 + (lane >> 4);
-    const int ch = (lane & 15) ^ swz_mn(krow);
-    const int gc = r0 + h * 128 + ch * 8;
-    p.kpos = krow;
-    p.off0 = gc < ext ? (uint32_t)(((long)krow * ld + gc) * 2) : kOOB;
-  }
-  return p;
-}
-
-// One 1-KiB piece.  dst is wave-uniform (SGPR math only); `tail` = this tile is the partial last
-// K-tile (per-lane k check, rare); t >= nk re-loads tile 0 into the sink (never read).
-MG_DEVICE void issue(char* dst, __amdgpu_buffer_rsrc_t rs, const Piece& pc, bool tail, int klim) {
-  uint32_t off = pc.off0;
-  if (tail) off = pc.kpos < klim ? off : kOOB;
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)dst, 16, off, 0, 0, 0);
-}
-}  // namespace ppk
-
-template <bool AK, bool BKC, int EPI, bool OUTF32>
-__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const GemmArgs args) {
-  using CF = Cfg<256, 256, 2, 4>;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
-
-  const int nblk = args.tiles_m * args.tiles_n * args.splits;
-  const int orig = blockIdx.x;
-  const int xcd = orig & 7, q8 = nblk >> 3, r8 = nblk & 7;
-  const int wgs = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int ntiles = args.tiles_m * args.tiles_n;
-  const int split = wgs / ntiles;
-  const int wg = wgs % ntiles;
-  const int group = GROUP_M * args.tiles_n;
-  const int first_m = (wg / group) * GROUP_M;
-  const int gm = min(args.tiles_m - first_m, GROUP_M);
-  const int m0 = (first_m + (wg % group) % gm) * 256;
-  const int n0 = ((wg % group) / gm) * 256;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int kbeg = split * args.kchunk;
-  const int nk = (min(args.K, kbeg + args.kchunk) - kbeg + BK - 1) / BK;
-  const int swid = __builtin_amdgcn_readfirstlane(wid);
-  const uint32_t sta = AK ? BK * 2 : (uint32_t)(BK * args.lda * 2);
-  const uint32_t stb = BKC ? BK * 2 : (uint32_t)(BK * args.ldb * 2);
-  // operand bases at the split's first k; extents from there
-  // k-contiguous operands carry the tile's row origin in the base (not in the 32-bit per-lane
-  // offsets), so operands past 4 GiB address correctly
-  const uint64_t a_k0 = AK ? ((uint64_t)m0 * args.lda + kbeg) * 2 : (uint64_t)kbeg * args.lda * 2;
-  const uint64_t b_k0 = BKC ? ((uint64_t)n0 * args.ldb + kbeg) * 2 : (uint64_t)kbeg * args.ldb * 2;
-  const char* abase = reinterpret_cast<const char*>(args.A) + a_k0;
-  const char* bbase = reinterpret_cast<const char*>(args.B) + b_k0;
-  const uint32_t abytes = (uint32_t)min<uint64_t>(args.a_bytes > a_k0 ? args.a_bytes - a_k0 : 0u, 0xFFFFFF00u);
-  const uint32_t bbytes = (uint32_t)min<uint64_t>(args.b_bytes > b_k0 ? args.b_bytes - b_k0 : 0u, 0xFFFFFF00u);
-  // k limit relative to the split start (ka/kb: reads as zero beyond), and the partial tile
-  const int kla = min(args.ka, kbeg + args.kchunk) - kbeg, klb = min(args.kb, kbeg + args.kchunk) - kbeg;
-  const int tail_t = min(kla, klb) / BK;  // first K-tile needing per-lane k checks (usually none)
-  ppk::Piece pa[2][2], pb[2][2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      pa[h][kh] = ppk::make_piece<AK>(args.lda, AK ? 0 : m0, AK ? args.a_ext - m0 : args.a_ext, h, kh, wid, lane);
-      pb[h][kh] = ppk::make_piece<BKC>(args.ldb, BKC ? 0 : n0, BKC ? args.b_ext - n0 : args.b_ext, h, kh, wid, lane);
-    }
-  auto dst_of = [&](int t, int opoff, int ro, int slot) -> char* {
-    return t < nk ? smem + (t & 1) * ppk::BUF + opoff + ro + swid * 1024
-                  : smem + ppk::SINK + slot * 8192 + swid * 1024;
-  };
-  // two pieces of one operand, K-tile t, k-half kh (h = 0, 1 -> sink slots 0, 1)
-  auto stage2A = [&](int t, int kh) {
-    const int tt = t < nk ? t : 0;
-    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(abase, abytes, sta, tt);
-    const bool tail = tt >= tail_t;
-    const int klim = kla - tt * BK;
-    ppk::issue(dst_of(t, 0, ppk::round_off<AK>(0, kh), 0), rs, pa[0][kh], tail, klim);
-    ppk::issue(dst_of(t, 0, ppk::round_off<AK>(1, kh), 1), rs, pa[1][kh], tail, klim);
-  };
-  auto stage2B = [&](int t, int kh) {
-    const int tt = t < nk ? t : 0;
-    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(bbase, bbytes, stb, tt);
-    const bool tail = tt >= tail_t;
-    const int klim = klb - tt * BK;
-    ppk::issue(dst_of(t, 32768, ppk::round_off<BKC>(0, kh), 0), rs, pb[0][kh], tail, klim);
-    ppk::issue(dst_of(t, 32768, ppk::round_off<BKC>(1, kh), 1), rs, pb[1][kh], tail, klim);
-  };
-  // prologue: tile 0 (K0 then K1), then tile 1's K0 rounds of A (window -1, phase 3)
-  stage2A(0, 0); stage2B(0, 0);
-  stage2A(0, 1); stage2B(0, 1);
-  stage2A(1, 0);
-  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs one barrier behind
-  asm volatile("" ::: "memory");
-
-  bf16x8 fa[4], fb[4];
-#ifdef MG_GEMM_STAMPS
-  unsigned long long st[4][6];
-#define PP_STAMP(p, k) if (W == MG_GEMM_STAMPS) st[p][k] = __builtin_amdgcn_s_memtime()
-#else
-#define PP_STAMP(p, k)
-#endif
-  for (int W = 0; W < nk; ++W) {
-    const char* sa = smem + (W & 1) * ppk::BUF;
-    const char* sbb = sa + 32768;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int ks = p >> 1, ih = p & 1;
-      PP_STAMP(p, 0);
-#ifndef MG_PP_NOREAD
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = ppk::frag<AK>(sa, wr * 8 + ih * 4 + i, ks, lane);
-      if (ih == 0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) fb[j] = ppk::frag<BKC>(sbb, wc * 4 + j, ks, lane);
-      }
-#else
-      if (W == 0 && p == 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { fa[i] = ppk::frag<AK>(sa, wr * 8 + i, 0, lane); fb[i] = ppk::frag<BKC>(sbb, wc * 4 + i, 0, lane); }
-      }
-#endif
-#ifndef MG_PP_NODMA
-      if (p == 0) stage2B(W + 1, 0);
-      if (p == 1) stage2A(W + 1, 1);
-      if (p == 2) stage2B(W + 1, 1);
-      if (p == 3) stage2A(W + 2, 0);
-#endif
-      PP_STAMP(p, 1);
-#ifndef MG_PP_NODMA
-      if (p == 1 || p == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-#endif
-      __builtin_amdgcn_sched_barrier(0);
-      PP_STAMP(p, 2);
-      __builtin_amdgcn_s_barrier();
-      PP_STAMP(p, 3);
-      lds_ready(fa);
-      lds_ready(fb, false);
-      __builtin_amdgcn_sched_barrier(0);
-      PP_STAMP(p, 4);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[ih * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[ih * 4 + i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      PP_STAMP(p, 5);
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
-  }
-#ifdef MG_GEMM_STAMPS
-  if (args.dbg && lane == 0 && nk > MG_GEMM_STAMPS)
-    for (int p = 0; p < 4; ++p)
-      for (int k = 0; k < 6; ++k) args.dbg[((long)blockIdx.x * 8 + wid) * 24 + p * 6 + k] = st[p][k];
-#endif
-#undef PP_STAMP
-  if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // sink DMA of the tail
-  __syncthreads();
-  epilogue<CF, EPI, OUTF32, ppk::SMEM / 8>(args, acc, m0, n0, wr, wc, wid, lane, smem);
 }
 
 // Split-K for the fp32-accumulate (weight-gradient) layout: pick the split that minimises
@@ -1130,23 +829,6 @@ static void set_split(GemmArgs& a, int slots, int ovh) {
   const int sp = choose_split(a.tiles_m * a.tiles_n, slots, nkt, ovh, spmin);
   a.kchunk = cdiv(nkt, sp) * BK;
   a.splits = cdiv(a.K, a.kchunk);
-}
-
-template <bool AK, bool BKC, int EPI, bool OUTF32>
-void launch_pp(GemmArgs a, hipStream_t stream) {
-  a.tiles_m = cdiv(a.M, 256);
-  a.tiles_n = cdiv(a.N, 256);
-  a.splits = 1;
-  a.kchunk = cdiv(a.K, BK) * BK;
-  if (OUTF32) set_split(a, 256, 6);
-  const int grid = a.tiles_m * a.tiles_n * a.splits;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)gemm_pp_kernel<AK, BKC, EPI, OUTF32>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, ppk::SMEM);
-    attr_set = true;
-  }
-  gemm_pp_kernel<AK, BKC, EPI, OUTF32><<<grid, 512, ppk::SMEM, stream>>>(a);
 }
 
 // ============================================================================================
@@ -1254,7 +936,6 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
   // the slot pattern every transposed read's slot offset is a constant in its offset field
   // (every layout: the all-k-contiguous forward gained +0.4 % of the step too, its slot bases then
   // fold into the reads' offsets; profiles/round4_w4_nt_unroll_ab.txt)
-  constexpr bool UNR = MG_W4_UNROLL;
   constexpr int AS = AK ? WK::A_SLOT : 16384, AHS = 2 * 16384;  // A: slot / half-image strides
   constexpr int BS = BKC ? WK::B_SLOT : 16384, BHS = 3 * 16384;  // B: 3 slots
   Stager<AK, 256, 4, AHS> sta;
@@ -1287,15 +968,20 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
   lds_ready(fb0, false);
   W4_STAMP(7);
 
-  // One K-tile with compile-time ring slots SA (A, kt & 1) and SB (B, kt % 3): the same schedule
-  // as the runtime-slot loop below (see it for the phase comments)
+  // One K-tile with compile-time ring slots SA (A, kt & 1) and SB (B, kt % 3), so every slot base
+  // is a constant in the LDS reads' offset fields and the K-loop below is unrolled over the 6-tile
+  // slot pattern
   auto ktile = [&](int kt, auto sa_c, auto sb_c) __attribute__((always_inline)) {
     constexpr int SA = decltype(sa_c)::value, SB = decltype(sb_c)::value;
     constexpr int OA = SA * AS, OA1 = (SA ^ 1) * AS;
     constexpr int OB = SB * BS, OB1 = ((SB + 1) % 3) * BS, OB2 = ((SB + 2) % 3) * BS;
     W4_KSTAMP(0);
     const int t2 = kt + 2;
+    // past the end: re-read a tile into a slot nobody reads (every K-tile waits with the same counts)
     const int tt = w4_tile(t2 < nk ? t2 : 1, nk, tail_first);
+    // phase A: k32 step 0 of tile kt; step-1 fragments read between the MFMAs (one per 2, B first:
+    // the next phase's first FN MFMAs use fa[0] with every fb[j]); B of tile kt+2 by DMA into B
+    // slot (kt+2) % 3
     {
       const __amdgpu_buffer_rsrc_t rb = stb.rsrc(tt);
 #pragma unroll
@@ -1310,81 +996,6 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
         if (w4_piece_at<NQ, WK::PB>(q) >= 0) stb.piece(sB + OB2, rb, tt, w4_piece_at<NQ, WK::PB>(q), false);
       }
     }
-    W4_KSTAMP(1);
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(WK::PB) : "memory");
-    lds_ready(fa1, false);
-    lds_ready(fb1, false);
-    W4_KSTAMP(2);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    W4_KSTAMP(3);
-    {
-      const __amdgpu_buffer_rsrc_t ra = sta.rsrc(tt);
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int i = q / FN, j = q % FN;
-        if (q == NQ - 1) mfma_acc_last(acc[i][j], fb1[j], fa1[i]);
-        else mfma_acc(acc[i][j], fb1[j], fa1[i]);
-        if (w4_piece_at<NQ, WK::PA>(q) >= 0) sta.piece(smem + OA, ra, tt, w4_piece_at<NQ, WK::PA>(q), false);
-        if (q < 2 * NR && (q & 1) == 1) {
-          const int r = q >> 1;
-          if (r < FN) fb0[r] = frag_k<BKC, 0, BHS, OB1>(sB, wn * FN + r, lane);
-          else fa0[r - FN] = frag_k<AK, 0, AHS, OA1>(smem, wm * 8 + r - FN, lane);
-        }
-      }
-    }
-    W4_KSTAMP(4);
-    lds_ready(fa0);
-    lds_ready(fb0, false);
-    W4_KSTAMP(5);
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-
-  if constexpr (UNR) {
-    // slot pattern of K-tiles 6n .. 6n + 5: (A, B) = (0,0) (1,1) (0,2) (1,0) (0,1) (1,2)
-    int kt = 0;
-    for (; kt + 6 <= nk; kt += 6) {
-      ktile(kt, I0{}, I0{});
-      ktile(kt + 1, I1{}, I1{});
-      ktile(kt + 2, I0{}, I2{});
-      ktile(kt + 3, I1{}, I0{});
-      ktile(kt + 4, I0{}, I1{});
-      ktile(kt + 5, I1{}, I2{});
-    }
-    if (kt < nk) ktile(kt, I0{}, I0{});
-    if (kt + 1 < nk) ktile(kt + 1, I1{}, I1{});
-    if (kt + 2 < nk) ktile(kt + 2, I0{}, I2{});
-    if (kt + 3 < nk) ktile(kt + 3, I1{}, I0{});
-    if (kt + 4 < nk) ktile(kt + 4, I0{}, I1{});
-  }
-  int bs = 0;  // B slot of tile kt (kt % 3)
-  for (int kt = 0; kt < (UNR ? 0 : nk); ++kt) {
-    W4_KSTAMP(0);
-    const int bs1 = bs == 2 ? 0 : bs + 1, bs2 = bs == 0 ? 2 : bs - 1;  // slots of kt+1, kt+2
-    const char* sa = smem + (kt & 1) * WK::A_SLOT;
-    const char* sb = sB + bs * WK::B_SLOT;
-    const int t2 = kt + 2;
-    const int tt = w4_tile(t2 < nk ? t2 : 1, nk, tail_first);  // past the end: re-read a tile into a slot nobody reads
-    // phase A: k32 step 0 of tile kt; step-1 fragments read between the MFMAs (one per 2); B of
-    // tile kt+2 by DMA into B slot (kt+2) % 3
-    {
-      const __amdgpu_buffer_rsrc_t rb = stb.rsrc(tt);
-      char* dstb = sB + bs2 * WK::B_SLOT;
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int i = q / FN, j = q % FN;
-        mfma_acc(acc[i][j], fb0[j], fa0[i]);
-        if ((q & 1) == 0 && q < 2 * NR) {
-          // B fragments first: the next phase's first FN MFMAs use fa[0] with every fb[j]
-          const int r = q >> 1;
-          if (r < FN) fb1[r] = frag_k<BKC, 1>(sb, wn * FN + r, lane);
-          else fa1[r - FN] = frag_k<AK, 1>(sa, wm * 8 + r - FN, lane);
-        }
-        if (w4_piece_at<NQ, WK::PB>(q) >= 0) stb.piece(dstb, rb, tt, w4_piece_at<NQ, WK::PB>(q), false);
-      }
-    }
     // tile kt+1 landed (this wave's DMA older than the B pieces just issued), every wave done
     // reading A slot kt & 1
     W4_KSTAMP(1);
@@ -1396,12 +1007,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
     asm volatile("" ::: "memory");
     W4_KSTAMP(3);
     // phase B: k32 step 1 of tile kt; A of tile kt+2 by DMA into A slot kt & 1; step-0 fragments
-    // of tile kt+1 between the MFMAs
+    // of tile kt+1 between the MFMAs, B first, early in the phase so they have ~3/4 of it to land
+    // before the next phase A needs them
     {
       const __amdgpu_buffer_rsrc_t ra = sta.rsrc(tt);
-      char* dsta = smem + (kt & 1) * WK::A_SLOT;
-      const char* sn = smem + ((kt + 1) & 1) * WK::A_SLOT;
-      const char* snb = sB + bs1 * WK::B_SLOT;
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
         const int i = q / FN, j = q % FN;
@@ -1409,13 +1018,11 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
         // duplicate the accumulator into other AGPRs; 16 cycles per 2048 is cheaper than that)
         if (q == NQ - 1) mfma_acc_last(acc[i][j], fb1[j], fa1[i]);
         else mfma_acc(acc[i][j], fb1[j], fa1[i]);
-        if (w4_piece_at<NQ, WK::PA>(q) >= 0) sta.piece(dsta, ra, tt, w4_piece_at<NQ, WK::PA>(q), false);
+        if (w4_piece_at<NQ, WK::PA>(q) >= 0) sta.piece(smem + OA, ra, tt, w4_piece_at<NQ, WK::PA>(q), false);
         if (q < 2 * NR && (q & 1) == 1) {
-          // fragment reads of tile kt+1 step 0, B first, early in the phase so they have ~3/4 of
-          // it to land before the next phase A needs them
           const int r = q >> 1;
-          if (r < FN) fb0[r] = frag_k<BKC, 0>(snb, wn * FN + r, lane);
-          else fa0[r - FN] = frag_k<AK, 0>(sn, wm * 8 + r - FN, lane);
+          if (r < FN) fb0[r] = frag_k<BKC, 0, BHS, OB1>(sB, wn * FN + r, lane);
+          else fa0[r - FN] = frag_k<AK, 0, AHS, OA1>(smem, wm * 8 + r - FN, lane);
         }
       }
     }
@@ -1423,8 +1030,26 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
     lds_ready(fa0);  // read early in phase B: long landed, the wait is free
     lds_ready(fb0, false);
     W4_KSTAMP(5);
-    bs = bs1;
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+
+  // slot pattern of K-tiles 6n .. 6n + 5: (A, B) = (0,0) (1,1) (0,2) (1,0) (0,1) (1,2)
+  int kt = 0;
+  for (; kt + 6 <= nk; kt += 6) {
+    ktile(kt, I0{}, I0{});
+    ktile(kt + 1, I1{}, I1{});
+    ktile(kt + 2, I0{}, I2{});
+    ktile(kt + 3, I1{}, I0{});
+    ktile(kt + 4, I0{}, I1{});
+    ktile(kt + 5, I1{}, I2{});
   }
+  if (kt < nk) ktile(kt, I0{}, I0{});
+  if (kt + 1 < nk) ktile(kt + 1, I1{}, I1{});
+  if (kt + 2 < nk) ktile(kt + 2, I0{}, I2{});
+  if (kt + 3 < nk) ktile(kt + 3, I1{}, I0{});
+  if (kt + 4 < nk) ktile(kt + 4, I0{}, I1{});
   W4_STAMP(8);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1482,14 +1107,11 @@ void launch(GemmArgs a, hipStream_t stream) {
   gemm_kernel<CF, AK, BKC, EPI, OUTF32><<<grid, CF::NT, CF::SMEM, stream>>>(a);
 }
 
-// Tile config per shape and layout, from bench/bench_gemm.py at the GPT-2 step shapes (M = 32768
-// tokens) and the 4096^3 / 8192^3 squares (profiles/round1_gemm_bench.jsonl):
-//   forward (NT):  W4 (1 wave/SIMD, 128x128 wave tiles) once there are >= 3 rounds of 256^2 tiles
-//                  or a long K; T128 for the small N = 768, K = 768 projection
-//   dgrad (NN), wgrad (TN): the ping-pong 256^2 kernel (PP) for long K or many tiles / large
-//                  weight-gradient outputs; T128 for 768 x 768
-// 256-tile kernels lose to T128 when a short K leaves prologue/epilogue dominant or when the tile
-// count quantises badly onto the 256 CUs.
+// Tile config per shape and layout (bench/bench_gemm.py, bench_wgrad.py, dgrad_nn_vs_nt.py):
+//   forward (NT):  W4 (256x256, or 256x192 where that quantises better onto the 256 CUs) once there
+//                  is at least one full round of 256^2 tiles; T128 below that (gpt-mini)
+//   dgrad (NN):    W4 from one round of 256^2 tiles up, T128 below
+//   wgrad (TN):    W4 or T128 through the split-K cost model (below)
 int pick_config(int M, int N, int K, int layout) {
   if (g_variant) return g_variant;
   const long tm = cdiv(M, 256);
@@ -1530,9 +1152,6 @@ template <bool AK, bool BKC, int EPI, bool OUTF32>
 void dispatch(const GemmArgs& a, hipStream_t stream) {
   const int layout = OUTF32 ? 2 : (BKC ? 0 : 1);
   switch (pick_config(a.M, a.N, a.K, layout)) {
-    case 2: launch<T256, AK, BKC, EPI, OUTF32>(a, stream); break;
-    case 3: launch<T2x1, AK, BKC, EPI, OUTF32>(a, stream); break;
-    case 4: launch_pp<AK, BKC, EPI, OUTF32>(a, stream); break;
     case 5: launch_w4<256, AK, BKC, EPI, OUTF32>(a, stream); break;
     case 6: launch_w4<192, AK, BKC, EPI, OUTF32>(a, stream); break;
     default: launch<T128, AK, BKC, EPI, OUTF32>(a, stream); break;
@@ -1543,7 +1162,10 @@ void dispatch(const GemmArgs& a, hipStream_t stream) {
 
 namespace mg {
 
-void gemm_set_variant(int v) { g_variant = v; }
+void gemm_set_variant(int v) {
+  if (v != 0 && v != 1 && v != 5 && v != 6) throw std::invalid_argument("gemm_set_variant: 0 (auto), 1 (T128), 5 (W4), 6 (W4 BN=192)");
+  g_variant = v;
+}
 void gemm_set_debug_buffer(unsigned long long* p) { g_dbg = p; }
 int gemm_get_variant() { return g_variant; }
 
@@ -1551,11 +1173,9 @@ int gemm_get_variant() { return g_variant; }
 void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long lda, long ldb,
           long ldc, int M, int N, int K, int a_ext, int b_ext, int ka, int kb, const bf16_t* bias,
           bf16_t* aux, const bf16_t* resid, float p, uint64_t seed, hipStream_t stream,
-          size_t a_bytes, size_t b_bytes, float* dbias, const GemmDelta* dl) {
+          size_t a_bytes, size_t b_bytes, float* dbias) {
   GemmArgs a;
   a.dbias = dbias;
-  a.delta = dl ? dl->delta : nullptr;
-  a.dT = dl ? dl->T : 1; a.dH = dl ? dl->H : 1; a.dhd = dl ? dl->hd : 8; a.drow0 = dl ? dl->row0 : 0;
   a.a_bytes = a_bytes;  // full sizes: each block's descriptor starts at its own tile / split origin
   a.b_bytes = b_bytes;
   a.A = A; a.B = B; a.C = C; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
@@ -1566,15 +1186,10 @@ void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long l
   a.tiles_m = a.tiles_n = a.splits = 1;
   a.kchunk = K;
   a.dbg = g_dbg;
-  {
-    // bf16 outputs are written non-temporally: they are consumed by a later kernel, and keeping
-    // them out of L2 / MALL leaves those to the GEMM operands (one-box A/B at B = 64: LM head
-    // forward 5.07 -> 4.51 ms; step +1.3 % with every output > 256 MB, +0.5 % more with all of
-    // them).  MINGPT_GEMM_NT_STORE=0 restores write-back stores.
-    static int nt = -1;
-    if (nt < 0) { const char* e = getenv("MINGPT_GEMM_NT_STORE"); nt = e ? atoi(e) : 1; }
-    a.nt_out = nt != 0;
-  }
+  // bf16 outputs are written non-temporally: they are consumed by a later kernel, and keeping them
+  // out of L2 / MALL leaves those to the GEMM operands (one-box A/B at B = 64: LM head forward
+  // 5.07 -> 4.51 ms; step +1.3 % with every output > 256 MB, +0.5 % more with all of them)
+  a.nt_out = 1;
   if (layout == 0) {
     if (epi == 0) dispatch<true, true, 0, false>(a, stream);
     else if (epi == 1) dispatch<true, true, 1, false>(a, stream);
@@ -1583,7 +1198,6 @@ void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long l
     else dispatch<true, true, 4, false>(a, stream);  // dgrad as NT against a transposed weight
   } else if (layout == 1) {
     if (epi == 4) dispatch<true, false, 4, false>(a, stream);
-    else if (epi == 5) dispatch<true, false, 5, false>(a, stream);
     else dispatch<true, false, 0, false>(a, stream);
   } else {
     dispatch<false, false, 0, true>(a, stream);

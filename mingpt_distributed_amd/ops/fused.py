@@ -18,8 +18,6 @@ fixed), embedding ``model.py:193-231``, head + loss ``model.py:309-320``.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 from . import gemm as G
@@ -39,20 +37,13 @@ def _bf16(t: torch.Tensor) -> torch.Tensor:
 
 # ------------------------------------------------------------------------------------ embedding
 
-# The MLP fc bias gradient summed inside the fc2 data-gradient GEMM's staged epilogue (one add per
-# stored element, one atomic per tile column) instead of a separate 400 MB column-sum pass over
-# dpre.  MINGPT_FC_DBIAS_FUSED=0 restores the separate bias_grad kernel.
-_FC_DBIAS_FUSED = os.environ.get("MINGPT_FC_DBIAS_FUSED", "1") == "1"
-# The qkv bias gradient summed inside the attention backward (dK / dV columns per key block in
-# registers, dQ columns in the dQ finalize) instead of a separate 300 MB pass over dqkv.
-# MINGPT_QKV_DBIAS_FUSED=0 restores the separate bias_grad kernel.
-_QKV_DBIAS_FUSED = os.environ.get("MINGPT_QKV_DBIAS_FUSED", "1") == "1"
-# MINGPT_DELTA_FUSED=1: the attention backward's delta = rowsum(dO * O) computed in the epilogue of
-# the GEMM that produces dO (gemm.hip epilogue 5) instead of attn_bwd_pre_kernel.  Off by default:
-# the K = 768 projection GEMM pays more for the fp32 staging and the O loads in its epilogue (282 vs
-# ~160 us at B = 128) than the separate 73 us pass costs (one-box A/B 1,006.0k / 995.0k fused vs
-# 1,007.7k / 998.8k, profiles/round2_s10_delta_epilogue_ab.txt).
-_DELTA_FUSED = os.environ.get("MINGPT_DELTA_FUSED", "0") == "1"
+# Decided (measured) fusions, no runtime switches: the MLP fc bias gradient is summed inside the fc2
+# data-gradient GEMM's staged epilogue (one add per stored element, one atomic per tile column; no
+# separate 400 MB column-sum pass over dpre), and the qkv bias gradient inside the attention backward
+# (dK / dV columns per key block in registers, dQ columns by one column-sum pass after the finalize).
+# The attention backward's delta = rowsum(dO * O) has its own pass (attn_bwd_pre_kernel): computing
+# it in the dO GEMM's epilogue cost the K = 768 projection more than the pass (round 2,
+# profiles/round2_s10_delta_epilogue_ab.txt).
 
 
 def _dgrad(dy, w):
@@ -149,11 +140,8 @@ class TransformerBlockFn(_EngineFn):
             dz = dx2
             C.bias_grad(dz, g[id(bp)][0])
         _wgrad(dz, u, g[id(wp)])
-        if _FC_DBIAS_FUSED:  # fc bias gradient: column sums of dpre in the GELU' epilogue
-            dpre = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=gd, dbias=g[id(bfc)][0])
-        else:
-            dpre = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=gd)
-            C.bias_grad(dpre, g[id(bfc)][0])
+        # fc bias gradient: column sums of dpre in the GELU' epilogue
+        dpre = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=gd, dbias=g[id(bfc)][0])
         _wgrad(dpre, h2, g[id(wfc)])
         dh2 = _dgrad(dpre, wfc)
         dx1 = C.layernorm_bwd(dh2, x1, ln2w, mean2, rstd2, g[id(ln2w)][0], g[id(ln2b)][0], dx2)
@@ -164,21 +152,10 @@ class TransformerBlockFn(_EngineFn):
             dz = dx1
             C.bias_grad(dz, g[id(bo)][0])
         _wgrad(dz, y, g[id(wo)])
-        hd = wo.shape[0] // H
-        delta = None
-        if _DELTA_FUSED and hd in (8, 16, 32, 64):
-            # the attention backward's rowsum(dO * O) in the dO GEMM's epilogue (no separate pass)
-            delta = torch.empty(B * H * T, dtype=torch.float32, device=dz.device)
-            dy = G.gemm_nn(dz, wo, epi="delta", aux=y, delta=(delta, T, H, hd))
-        else:
-            dy = _dgrad(dz, wo)
-        if _QKV_DBIAS_FUSED:  # qkv bias gradient summed inside the attention backward
-            dqkv = C.attention_bwd(qkv, y, dy, lse, amask, B, T, H, float(p_attn), ctx.seeds[0],
-                                   g[id(bqkv)][0], delta)
-        else:
-            dqkv = C.attention_bwd(qkv, y, dy, lse, amask, B, T, H, float(p_attn), ctx.seeds[0],
-                                   None, delta)
-            C.bias_grad(dqkv, g[id(bqkv)][0])
+        dy = _dgrad(dz, wo)
+        # qkv bias gradient summed inside the attention backward
+        dqkv = C.attention_bwd(qkv, y, dy, lse, amask, B, T, H, float(p_attn), ctx.seeds[0],
+                               g[id(bqkv)][0], None)
         _wgrad(dqkv, h, g[id(wqkv)])
         dh = _dgrad(dqkv, wqkv)
         dx = C.layernorm_bwd(dh, x, ln1w, mean1, rstd1, g[id(ln1w)][0], g[id(ln1b)][0], dx1)
@@ -191,8 +168,7 @@ class TransformerBlockFn(_EngineFn):
 # gradient ([M, 50304] x [50304, 768]: the 128x96-wave W4 tile) and weight gradient (fp32
 # accumulate into main_grad) all run on gemm.hip.  Training cross-entropy in one pass over the
 # logits (xent.hip xent_fused: loss and dlogits = (softmax - onehot) / n_valid written in forward,
-# grad_out applied in backward).  MINGPT_XENT_FUSED=0 keeps the two-pass fwd / bwd kernels.
-_XENT_FUSED = os.environ.get("MINGPT_XENT_FUSED", "1") == "1"
+# grad_out applied in backward); without gradients (evaluation) the loss-only xent_fwd pass.
 
 
 class HeadLossFn(_EngineFn):
@@ -206,7 +182,7 @@ class HeadLossFn(_EngineFn):
         ld = (V + 127) // 128 * 128
         h, mean, rstd = C.layernorm_fwd(x, lnw, lnb, eps)
         logits = G.gemm_nt(h, w, ld=ld)
-        fused = C.xent_fused(logits, targets, V) if _XENT_FUSED and any(ctx.needs_input_grad) else []
+        fused = C.xent_fused(logits, targets, V) if any(ctx.needs_input_grad) else []
         if fused:  # the backward never reads the logits again
             out, dlogits = fused
             ctx.save_for_backward(x, h, mean, rstd, dlogits, None, None, out)

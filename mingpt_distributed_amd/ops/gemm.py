@@ -10,33 +10,30 @@ epilogue fused where the data is produced.
 * ``gemm_tn_acc``  C[N,K] += A[M,N]^T @ B[M,K] (weight gradient, fp32 accumulate into main_grad)
 
 All three run on the hand-written MFMA kernels in ``csrc/kernels/gemm.hip`` (``_C.gemm``); the
-training step (``ops/fused.py``) uses nothing else by default (``MINGPT_*_BLAS=1`` switches route
-some plain GEMMs to hipBLASLt, see its module docstring).
+training step (``ops/fused.py``) uses nothing else, and there is no runtime switch to a library
+GEMM (hipBLASLt is only a reference point in ``bench/gemm_blas_shapes.py``).
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
 
 from ._ext import ext
 
-EPI_NONE, EPI_BIAS, EPI_GELU, EPI_RESID, EPI_GELU_BWD, EPI_DELTA = 0, 1, 2, 3, 4, 5
+EPI_NONE, EPI_BIAS, EPI_GELU, EPI_RESID, EPI_GELU_BWD = 0, 1, 2, 3, 4
 
 
 # Row-chunked launches are no longer needed for operands past 4 GiB (the GPT-2 logits beyond ~42k
 # tokens): each block's buffer descriptor starts at its own tile / split origin and split-K ranges
 # stay below 4 GiB (gemm.hip set_split).  The mechanism stays for tests (monkeypatch this cap).
 _MAX_BYTES = 1 << 62
-# data gradients NN from the stored weight (MINGPT_DGRAD_NN=0: NT against a transposed copy)
-_DGRAD_NN = os.environ.get("MINGPT_DGRAD_NN", "1") == "1"
 
 
 def _row_chunks(M: int, *row_bytes: int):
     """Row ranges [r0, r1) of an M-row operand such that no chunk of any operand whose rows are
     ``row_bytes`` wide reaches ``_MAX_BYTES``: the M-chunked launches are exact (the epilogues used
-    here do not depend on the global row index, the delta epilogue takes its row offset)."""
+    here do not depend on the global row index)."""
     cap = max(256, (_MAX_BYTES // max(max(row_bytes), 1)) // 256 * 256)
     if M <= cap:
         return [(0, M)]
@@ -92,7 +89,7 @@ def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, *, epi: str = "none",
     bench/dgrad_nn_vs_nt.py); a long reduction (the LM head's K = vocab) runs NT against W^T, where
     the 128x96-wave W4 tile applies.  With ``epi="gelu_bwd"`` and ``dbias`` (fp32 [N_in]), the
     column sums of the result (the next bias gradient) are accumulated in the epilogue."""
-    if _DGRAD_NN and wt is None and dy.shape[1] < 8192 and w.shape[0] == dy.shape[1]:
+    if wt is None and dy.shape[1] < 8192 and w.shape[0] == dy.shape[1]:
         return gemm_nn(dy, w, epi=epi, aux=aux, dbias=dbias)
     if wt is None:
         wt = transpose(w, dy.shape[1])
@@ -100,32 +97,21 @@ def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, *, epi: str = "none",
 
 
 def gemm_nn(a: torch.Tensor, b: torch.Tensor, *, epi: str = "none",
-            aux: Optional[torch.Tensor] = None, dbias: Optional[torch.Tensor] = None,
-            delta: Optional[tuple] = None) -> torch.Tensor:
+            aux: Optional[torch.Tensor] = None, dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """C = A @ B (B row-major [K, N]); ``gelu_bwd`` multiplies by ``aux`` (a stored GELU') and,
-    with ``dbias`` (fp32 [N]), adds the column sums of the stored C into it (staged epilogue).
-    ``delta`` epilogue (``delta=(out, T, H, hd)``, hd in {8, 16, 32, 64}): C is the attention
-    output's gradient dO and ``aux`` the attention output O; writes the attention backward's
-    out[(b H + h) T + t] = sum_d dO * O per head (fp32 products of the unrounded dO)."""
+    with ``dbias`` (fp32 [N]), adds the column sums of the fp32 C into it (staged epilogue)."""
     _check2d(a, "A")
     _check2d(b, "B")
     M, K = a.shape
     N = b.shape[1]
     c = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
-    code = {"none": EPI_NONE, "gelu_bwd": EPI_GELU_BWD, "delta": EPI_DELTA}[epi]
+    code = {"none": EPI_NONE, "gelu_bwd": EPI_GELU_BWD}[epi]
     if dbias is not None and code != EPI_GELU_BWD:
         raise ValueError("gemm_nn: dbias is fused only into the gelu_bwd epilogue")
-    if (code == EPI_DELTA) != (delta is not None):
-        raise ValueError("gemm_nn: the delta epilogue takes delta=(out, T, H, hd)")
-    dkw = {}
-    if delta is not None:
-        out, T, H, hd = delta
-        dkw = dict(delta=out, dT=int(T), dH=int(H), dhd=int(hd))
     chunks = _row_chunks(M, 2 * K, 2 * N)
     for r0, r1 in chunks:
         sl = (lambda t: t if t is None or len(chunks) == 1 else t[r0:r1])
-        ext().gemm(sl(a), b, sl(c), 1, code, None, sl(aux), None, 0.0, 0, r1 - r0, N, dbias,
-                   **(dict(dkw, row0=r0) if dkw else {}))
+        ext().gemm(sl(a), b, sl(c), 1, code, None, sl(aux), None, 0.0, 0, r1 - r0, N, dbias)
     return c
 
 

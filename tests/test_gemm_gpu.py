@@ -9,7 +9,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.fixture(autouse=True, params=[0, 1, 2, 3, 4, 5, 6], ids=["auto", "t128", "t256", "t256x128", "pp256", "w4", "w4n192"])
+@pytest.fixture(autouse=True, params=[0, 1, 5, 6], ids=["auto", "t128", "w4", "w4n192"])
 def tile_config(request):
     """Run every GEMM test under each tile configuration of gemm.hip (0 = per-shape choice)."""
     from mingpt_distributed_amd.ops._ext import ext
@@ -176,22 +176,6 @@ def test_row_chunked_launches_match(monkeypatch):
                                atol=1e-3, rtol=1e-4)
 
 
-@pytest.mark.parametrize("M,T,hd", [(1000, 250, 64), (8192, 1024, 64), (4096, 512, 32), (2048, 256, 16)])
-def test_dgrad_delta_epilogue(M, T, hd):
-    """Epilogue 5: the dO GEMM (dO = dZ Wo) also writes the attention backward's
-    delta[(b H + h) T + t] = sum_d dO * O per head (O = aux); T128 (partial tiles) and W4 shapes."""
-    D = 768
-    H = D // hd
-    dz, wo, y = _bf(M, D, seed=31), _bf(D, D, seed=32, scale=0.05), _bf(M, D, seed=33)
-    delta = torch.full((M // T * H * T,), float("nan"), device=DEV)
-    dy = G.gemm_nn(dz, wo, epi="delta", aux=y, delta=(delta, T, H, hd))
-    ref = dz.float() @ wo.float()
-    _check(dy, ref, D)
-    dref = (ref * y.float()).view(M // T, T, H, hd).sum(-1).permute(0, 2, 1).reshape(-1)
-    torch.testing.assert_close(delta, dref, atol=2e-2, rtol=1e-2)
-    torch.testing.assert_close(dy, G.gemm_nn(dz, wo), atol=0, rtol=0)  # the stored dO is unchanged
-
-
 def test_operands_past_4gib_single_launch(monkeypatch):
     """Operands past 4 GiB (the GPT-2 logits and their gradient beyond ~42k tokens) run as ONE
     launch: every block's buffer descriptor starts at its own tile / split origin, split-K ranges
@@ -215,3 +199,13 @@ def test_operands_past_4gib_single_launch(monkeypatch):
     # and the rows past 4 GiB really are read: the last 512 rows' logits against fp32 torch
     ref = h[-512:].float() @ w.float().t()
     torch.testing.assert_close(logits[-512:].float(), ref, atol=2e-2, rtol=2e-2)
+
+
+def test_deleted_tile_configs_are_rejected(tile_config):
+    """Only reachable configurations can be forced (2-4 were deleted in round 5)."""
+    from mingpt_distributed_amd.ops._ext import ext
+
+    for v in (2, 3, 4, 7):
+        with pytest.raises(Exception):
+            ext().gemm_set_variant(v)
+    ext().gemm_set_variant(tile_config)
