@@ -45,6 +45,9 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int BK = 64;
+#ifndef MG_GEMM_DIRECT_MAX
+#define MG_GEMM_DIRECT_MAX -1  // W4 bf16 epilogues EPI <= this on whole tiles: epilogue_direct (experiment)
+#endif
 #ifndef MG_GROUP_M
 #define MG_GROUP_M 8
 #endif
@@ -558,6 +561,165 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
   }
 }
 
+// ---- Direct epilogue (whole wave tiles, bf16 outputs): no LDS round trip.  The fragment layout
+// gives lane (row r = lane & 15, group g = lane >> 4) columns 16 j + 4 g .. +3 of fragment j; one
+// v_permlane16_swap per dword exchanges rows 1 / 3 of fragment j's registers with rows 0 / 2 of
+// fragment j+1's (guide T21 with 16-lane rows), after which the lane holds 8 consecutive columns:
+// fragment j + (g & 1), columns 8 (g >> 1) .. +7 -- one 16-byte store, and the four lanes of a row
+// cover 64 contiguous bytes per wave-instruction (16 rows x 64 B; the HBM access granule, unlike the
+// 32-byte row pieces of the fragment-direct stores measured in round 3).  fp32 values are swapped
+// (4 per pair) where a 16-byte side input must be applied before the bf16 rounding.
+MG_DEVICE uint32_t pl16_lo(uint32_t& x, uint32_t& y) {
+  const auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+  x = r[0];
+  y = r[1];
+  return x;
+}
+MG_DEVICE void pl16(float& x, float& y) {
+  uint32_t a = __float_as_uint(x), b = __float_as_uint(y);
+  pl16_lo(a, b);
+  x = __uint_as_float(a);
+  y = __uint_as_float(b);
+}
+
+template <class CF, int EPI>
+MG_DEVICE void epilogue_direct(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int m0, int n0, int wm,
+                               int wn, int lane_in, char* smem) {
+  int lane = lane_in;
+  static_assert(CF::FN % 2 == 0, "fragment pairs");
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  asm volatile("" : "+v"(lane));  // lane-derived addresses computed here, not hoisted into the K-loop
+  const int r = lane & 15, g = lane >> 4;
+  const int nw = n0 + wn * CF::WTN;
+  const int mw = m0 + wm * CF::WTM;
+  const int nb = nw + 4 * g;  // pre-swap columns of fragment j: nb + 16 j .. +3
+  const int cpost = 16 * (g & 1) + 8 * (g >> 1);  // post-swap column of fragment pair jp: 32 jp + cpost
+  uint2 bs[CF::FN];
+#pragma unroll
+  for (int j = 0; j < CF::FN; ++j) {
+    bs[j] = make_uint2(0u, 0u);
+    if constexpr (EPI == 1 || EPI == 2 || EPI == 3)
+      if (args.bias) bs[j] = *reinterpret_cast<const uint2*>(args.bias + nb + j * 16);
+  }
+  const uint32_t dkey = EPI == 3 ? rowdrop_key(eff_seed(args.seed, args.sofs)) : 0u;
+  const long off0 = (long)(mw + r) * args.ldc + nw + cpost;
+  bf16_t* gc = reinterpret_cast<bf16_t*>(args.C) + off0;
+  bf16_t* ga = EPI == 2 ? args.aux + off0 : nullptr;
+  const bf16_t* gr = EPI == 3 ? args.resid + off0 : EPI == 4 ? args.aux + off0 : nullptr;
+  const long rs = 16L * args.ldc;
+  float cs[EPI == 4 ? 4 * CF::FN : 1];  // EPI 4: this lane's column sums, [pair][8 columns]
+#pragma unroll
+  for (int k = 0; k < (EPI == 4 ? 4 * CF::FN : 1); ++k) cs[k] = 0.f;
+#pragma unroll
+  for (int i = 0; i < CF::FM; ++i) {
+    const int m = mw + 16 * i + r;
+    uint4 side[CF::FN / 2];
+    if constexpr (EPI == 3 || EPI == 4) {  // this row group's side pieces first: their latency under the math
+#pragma unroll
+      for (int jp = 0; jp < CF::FN / 2; ++jp) side[jp] = *reinterpret_cast<const uint4*>(gr + i * rs + 32 * jp);
+    }
+#pragma unroll
+    for (int jp = 0; jp < CF::FN / 2; ++jp) {
+      float v0[4], v1[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v0[e] = acc[i][2 * jp][e];
+        v1[e] = acc[i][2 * jp + 1][e];
+      }
+      if constexpr (EPI == 1 || EPI == 2 || EPI == 3) {
+        const uint2 b0 = bs[2 * jp], b1 = bs[2 * jp + 1];
+        v0[0] += bf2f(b0.x & 0xffffu); v0[1] += bf2f(b0.x >> 16); v0[2] += bf2f(b0.y & 0xffffu); v0[3] += bf2f(b0.y >> 16);
+        v1[0] += bf2f(b1.x & 0xffffu); v1[1] += bf2f(b1.x >> 16); v1[2] += bf2f(b1.y & 0xffffu); v1[3] += bf2f(b1.y >> 16);
+      }
+      if constexpr (EPI == 3 || EPI == 4) {
+        if constexpr (EPI == 3) {
+          if (args.thr) {
+            rowdrop4(v0, dkey, m, nb + 32 * jp, args.N, args.thr, args.scale);
+            rowdrop4(v1, dkey, m, nb + 32 * jp + 16, args.N, args.thr, args.scale);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pl16(v0[e], v1[e]);  // now v0 | v1 = 8 consecutive columns
+        const uint4 sv = side[jp];
+        const uint32_t w[4] = {sv.x, sv.y, sv.z, sv.w};
+        float o[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float sk = bf2f((w[k >> 1] >> (16 * (k & 1))) & 0xffffu);
+          o[k] = EPI == 3 ? o[k] + sk : o[k] * sk;
+        }
+        if constexpr (EPI == 4) {  // bias gradient: fp32 column sums before the bf16 rounding
+#pragma unroll
+          for (int k = 0; k < 8; ++k) cs[jp * 8 + k] += o[k];
+        }
+        const uint4 y = pack8(o);
+        __builtin_nontemporal_store(v4u{y.x, y.y, y.z, y.w}, reinterpret_cast<v4u*>(gc + i * rs + 32 * jp));
+      } else {
+        uint32_t gx0 = 0, gy0 = 0, gx1 = 0, gy1 = 0;
+        if constexpr (EPI == 2) {  // y = GELU(z) stored as C; GELU'(z) into aux
+          f32x2 ya, yb, ga0, gb0, yc, yd, gc0, gd0;
+          gelu2(f32x2{v0[0], v0[1]}, ya, ga0);
+          gelu2(f32x2{v0[2], v0[3]}, yb, gb0);
+          gelu2(f32x2{v1[0], v1[1]}, yc, gc0);
+          gelu2(f32x2{v1[2], v1[3]}, yd, gd0);
+          v0[0] = ya.x; v0[1] = ya.y; v0[2] = yb.x; v0[3] = yb.y;
+          v1[0] = yc.x; v1[1] = yc.y; v1[2] = yd.x; v1[3] = yd.y;
+          gx0 = pack2(ga0.x, ga0.y); gy0 = pack2(gb0.x, gb0.y);
+          gx1 = pack2(gc0.x, gc0.y); gy1 = pack2(gd0.x, gd0.y);
+        }
+        uint32_t x0 = pack2(v0[0], v0[1]), y0 = pack2(v0[2], v0[3]);
+        uint32_t x1 = pack2(v1[0], v1[1]), y1 = pack2(v1[2], v1[3]);
+        pl16_lo(x0, x1);
+        pl16_lo(y0, y1);
+        __builtin_nontemporal_store(v4u{x0, y0, x1, y1}, reinterpret_cast<v4u*>(gc + i * rs + 32 * jp));
+        if constexpr (EPI == 2) {
+          pl16_lo(gx0, gx1);
+          pl16_lo(gy0, gy1);
+          __builtin_nontemporal_store(v4u{gx0, gy0, gx1, gy1}, reinterpret_cast<v4u*>(ga + i * rs + 32 * jp));
+        }
+      }
+    }
+    // one row group at a time: without the fence the scheduler hoists every row group's
+    // accumulator reads (256 AGPR -> VGPR copies) to the top and the epilogue spills
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (EPI == 4) {
+    if (args.dbias) {  // kernel argument: uniform over the workgroup
+      // the 16 lanes of a column group (lane bits 0-3 = rows) fold by transposing shuffles: lane
+      // (r, g) keeps sums 2 r, 2 r + 1 of its 4 FN values (pair r / 4, columns 2 (r % 4) + j); the
+      // NWM row-waves meet in LDS (free once this wave's trailing DMA pieces have landed), then one
+      // atomic per tile column
+      constexpr int NV = 4 * CF::FN;
+#pragma unroll
+      for (int M = 8; M >= 1; M >>= 1) {
+        const bool hi = lane & M;
+        const int C = NV * M / 8;  // values still held before this step
+#pragma unroll
+        for (int i2 = 0; i2 < C / 2; ++i2) {
+          const float send = hi ? cs[i2] : cs[i2 + C / 2];
+          const float keep = hi ? cs[i2 + C / 2] : cs[i2];
+          cs[i2] = keep + __shfl_xor(send, M, 64);
+        }
+      }
+      float* red = reinterpret_cast<float*>(smem);  // [NWM][BN]
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < NV / 16; ++j) {
+        const int idx = (NV / 16) * r + j, jp = idx / 8, k = idx % 8;
+        red[wm * CF::BN + wn * CF::WTN + 32 * jp + cpost + k] = cs[j];
+      }
+      __syncthreads();
+      for (int c = threadIdx.x; c < CF::BN; c += CF::NT) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < CF::NWM; ++q) t += red[q * CF::BN + c];
+        atomicAdd(args.dbias + n0 + c, t);
+      }
+    }
+  }
+}
+
 // Shared epilogue: lane holds acc[i][j] = C[m0+wm*WTM+16i+(lane&15)][n0+wn*WTN+16j+4(lane>>4) .. +3].
 // LDSW: LDS bytes each wave may use for the staged form (the K-loop's buffers are free by then).
 template <class CF, int EPI, bool OUTF32, int LDSW>
@@ -1051,6 +1213,14 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
   if (kt + 3 < nk) ktile(kt + 3, I1{}, I0{});
   if (kt + 4 < nk) ktile(kt + 4, I0{}, I1{});
   W4_STAMP(8);
+  if constexpr (!OUTF32 && EPI <= MG_GEMM_DIRECT_MAX) {
+    const int nlim = EPI == 0 ? (int)args.ldc : args.N;
+    if (n0 + BN <= nlim && m0 + 256 <= args.M) {  // block-uniform: whole tile
+      epilogue_direct<CF, EPI>(args, acc, m0, n0, wm, wn, lane, smem);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA pieces past the last K-tile
+      return;
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 #ifdef MG_GEMM_EPI_STAMPS

@@ -155,7 +155,7 @@ class TransformerBlockFn(_EngineFn):
         dy = _dgrad(dz, wo)
         # qkv bias gradient summed inside the attention backward
         dqkv = C.attention_bwd(qkv, y, dy, lse, amask, B, T, H, float(p_attn), ctx.seeds[0],
-                               g[id(bqkv)][0], None)
+                               g[id(bqkv)][0])
         _wgrad(dqkv, h, g[id(wqkv)])
         dh = _dgrad(dqkv, wqkv)
         dx = C.layernorm_bwd(dh, x, ln1w, mean1, rstd1, g[id(ln1w)][0], g[id(ln1b)][0], dx1)

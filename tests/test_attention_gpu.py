@@ -76,22 +76,6 @@ def test_attention_bwd_fused_bias_grad(B, T, H, hd, p):
     torch.testing.assert_close(db, ref, atol=tol, rtol=2e-3)
 
 
-def test_attention_bwd_precomputed_delta():
-    """attention_bwd(..., delta=rowsum(dO * O)) (the dO GEMM's epilogue 5 computes it) skips its
-    own delta pass and gives the same gradients."""
-    C = ext()
-    B, T, H, hd = 2, 512, 3, 64
-    torch.manual_seed(3)
-    D = H * hd
-    qkv = torch.randn(B * T, 3 * D, device=DEV).to(torch.bfloat16)
-    out, lse, mask = C.attention_fwd(qkv, B, T, H, 0.1, 9)
-    dout = torch.randn(B * T, D, device=DEV).to(torch.bfloat16)
-    ref = C.attention_bwd(qkv, out, dout, lse, mask, B, T, H, 0.1, 9)
-    delta = (dout.float() * out.float()).view(B, T, H, hd).sum(-1).permute(0, 2, 1).contiguous().view(-1)
-    got = C.attention_bwd(qkv, out, dout, lse, mask, B, T, H, 0.1, 9, None, delta)
-    torch.testing.assert_close(got.float(), ref.float(), atol=2e-2, rtol=2e-2)
-
-
 def test_attention_causality():
     """Perturbing token j must not change outputs at positions < j (reference defect D4)."""
     C = ext()
