@@ -52,9 +52,12 @@ std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const at::Tensor& w, 
   return {y, mean, rstd};
 }
 
-at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
-                         const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& dw,
-                         const at::Tensor& db, const c10::optional<at::Tensor>& dres) {
+// drop_p > 0 with dz_bias (fp32 [D]): returns (dx, dz), dz = the residual-dropout backward of dx
+// (seed: the forward's) and dz's column sums added into dz_bias (layernorm.hip, fused)
+std::vector<at::Tensor> layernorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                                      const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& dw,
+                                      const at::Tensor& db, const c10::optional<at::Tensor>& dres,
+                                      const c10::optional<at::Tensor>& dz_bias, double drop_p, int64_t drop_seed) {
   CHECK_BF16(dy); CHECK_BF16(x); CHECK_BF16(w); CHECK_F32(mean); CHECK_F32(rstd);
   CHECK_F32(dw); CHECK_F32(db); CHECK_CONTIG(dy); CHECK_CONTIG(x);
   const int64_t D = x.size(-1), M = x.numel() / D;
@@ -66,10 +69,25 @@ at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Te
     CHECK_BF16(*dres); CHECK_CONTIG(*dres);
     TORCH_CHECK(dres->numel() == x.numel(), "layernorm_bwd: dres shape");
   }
+  const bool drop = dz_bias.has_value() && dz_bias->defined();
+  at::Tensor dz;
+  if (drop) {
+    CHECK_F32(*dz_bias); CHECK_CONTIG(*dz_bias);
+    TORCH_CHECK(dz_bias->numel() == D && D % 8 == 0, "layernorm_bwd: dz_bias must be fp32 [D]");
+    dz = at::empty_like(x);
+  }
   auto ws = at::empty({(int64_t)mg::layernorm_bwd_workspace((int)M, (int)D)}, mean.options());
   mg::layernorm_bwd(bp(dy), bp(x), bp(w), fp(mean), fp(rstd), bp_opt(dres), bp(dx), fp(dw), fp(db), fp(ws),
-                    (int)M, (int)D, cur_stream());
-  return dx;
+                    (int)M, (int)D, cur_stream(), drop ? bp(dz) : nullptr, drop ? fp(*dz_bias) : nullptr,
+                    (float)drop_p, (uint64_t)drop_seed);
+  if (drop) return {dx, dz};
+  return {dx};
+}
+
+at::Tensor layernorm_bwd_plain(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                               const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& dw,
+                               const at::Tensor& db, const c10::optional<at::Tensor>& dres) {
+  return layernorm_bwd(dy, x, w, mean, rstd, dw, db, dres, c10::nullopt, 0.0, 0)[0];
 }
 
 // ------------------------------------------------------------------------------- embedding
@@ -631,7 +649,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("comm_query", &mg::comm::query);
   m.doc() = "mingpt_distributed_amd gfx950 kernels";
   m.def("layernorm_fwd", &layernorm_fwd);
-  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("layernorm_bwd", &layernorm_bwd_plain);
+  m.def("layernorm_bwd_dropout", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"),
+        py::arg("rstd"), py::arg("dw"), py::arg("db"), py::arg("dres"), py::arg("dz_bias"),
+        py::arg("drop_p"), py::arg("drop_seed"));
   m.def("embedding_fwd", &embedding_fwd, py::arg("idx"), py::arg("wte"), py::arg("wpe"), py::arg("p"),
         py::arg("seed"), py::arg("pos_dev") = py::none(), py::arg("am_part") = py::none(),
         py::arg("seq") = py::none());

@@ -12,9 +12,12 @@ typedef uint16_t bf16_t;
 // layernorm.hip
 void layernorm_fwd(const bf16_t* x, const bf16_t* w, const bf16_t* b, bf16_t* y, float* mean,
                    float* rstd, int M, int D, float eps, hipStream_t stream);
+// dz (optional): also dz = residual-dropout backward of the stored dx (probability p, the forward's
+// seed), its fp32 column sums added into dzb (the bias gradient of the branch that produced x)
 void layernorm_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const float* mean,
                    const float* rstd, const bf16_t* dres, bf16_t* dx, float* dw, float* db,
-                   float* workspace, int M, int D, hipStream_t stream);
+                   float* workspace, int M, int D, hipStream_t stream, bf16_t* dz = nullptr,
+                   float* dzb = nullptr, float p = 0.f, uint64_t seed = 0);
 size_t layernorm_bwd_workspace(int M, int D);
 
 // embedding.hip

@@ -86,7 +86,21 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
-template <int NV>
+// DROP: the residual-dropout backward of the branch that produced this LN's input is fused in
+// (the consumer of dx in the step: /root/reference/mingpt/model.py:187-188's residual adds).  Besides
+// dx, the kernel writes dz = dropout'(bf16(dx)) (the same 16-bit mask as the forward's GEMM
+// epilogue, common.h rowdrop8) and accumulates dz's fp32 column sums -- the branch's bias gradient
+// -- into a third partial row; the separate dropout_bias_grad pass (one more 2-byte read per
+// element) is gone.
+struct LnDrop {
+  bf16_t* dz;
+  uint64_t seed;
+  const uint64_t* sofs;
+  uint32_t thr;
+  float scale;
+};
+
+template <int NV, bool DROP>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy,
                                                      const bf16_t* __restrict__ x,
                                                      const bf16_t* __restrict__ w,
@@ -94,8 +108,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
                                                      const float* __restrict__ rstd,
                                                      const bf16_t* __restrict__ dres,
                                                      bf16_t* __restrict__ dx,
-                                                     float* __restrict__ part, int M, int D) {
+                                                     float* __restrict__ part, int M, int D, const LnDrop dr) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  constexpr int NP = DROP ? 3 : 2;  // partial row: [dgamma | dbeta (| dbias)]
+  float zacc[DROP ? NV : 1][8];
+#pragma unroll
+  for (int i = 0; i < (DROP ? NV : 1); ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) zacc[i][j] = 0.f;
+  const uint64_t dseed = DROP ? eff_seed(dr.seed, dr.sofs) : 0;
   // rows are held PACKED (bf16 x 8 per uint4) between load and use: two rows of x, dy and the
   // residual gradient in flight cost 3 x 2 x NV x 4 registers instead of twice that as floats
   // (NV = 4, gpt2-xl's D = 1600, had 504 registers -> one wave per SIMD)
@@ -183,7 +204,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
             for (int j = 0; j < 8; ++j) o[j] += rv[j];
           }
-          st16(dxr + c, pack8(o));
+          const uint4 packed = pack8(o);
+          st16(dxr + c, packed);
+          if constexpr (DROP) {  // dz = dropout'(stored dx), its column sums (fp32)
+            float z[8];
+            unpack8(packed, z);
+            rowdrop8(z, dseed, row, c, D, dr.thr, dr.scale);
+            st16(dr.dz + row * D + c, pack8(z));
+#pragma unroll
+            for (int j = 0; j < 8; ++j) zacc[i][j] += z[j];
+          }
         }
       }
     }
@@ -191,44 +221,47 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
   // fold the 4 waves' column partials through LDS and store the block's partial row
   // [dgamma | dbeta] with plain stores; ln_colsum_kernel adds the blocks up (a single-stage
   // atomic fold put every block's atomics on the same 2D addresses)
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [4][2*D]
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [4][NP*D]
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = (i * 64 + lane) * 8;
     if (c < D) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        red[wid * 2 * D + c + j] = gacc[i][j];
-        red[wid * 2 * D + D + c + j] = bacc[i][j];
+        red[wid * NP * D + c + j] = gacc[i][j];
+        red[wid * NP * D + D + c + j] = bacc[i][j];
+        if constexpr (DROP) red[wid * NP * D + 2 * D + c + j] = zacc[i][j];
       }
     }
   }
   __syncthreads();
-  float* prow = part + (long)blockIdx.x * 2 * D;
-  for (int c = threadIdx.x; c < 2 * D; c += 256)
-    prow[c] = red[c] + red[2 * D + c] + red[4 * D + c] + red[6 * D + c];
+  float* prow = part + (long)blockIdx.x * NP * D;
+  for (int c = threadIdx.x; c < NP * D; c += 256)
+    prow[c] = red[c] + red[NP * D + c] + red[2 * NP * D + c] + red[3 * NP * D + c];
 }
 
 // dw += sum over blocks of part[:, :D], db += ... part[:, D:].  Block = 64 columns x 4 waves over a
 // 32-row chunk of the G partial rows (8 independent loads per lane: latency, not bandwidth, is
 // what this pass pays); one atomic per column per block (G / 32 per address).
-__global__ __launch_bounds__(256) void ln_colsum_kernel(const float* __restrict__ part, int G, int D,
-                                                        float* __restrict__ dw, float* __restrict__ db) {
+__global__ __launch_bounds__(256) void ln_colsum_kernel(const float* __restrict__ part, int G, int D, int NP,
+                                                        float* __restrict__ dw, float* __restrict__ db,
+                                                        float* __restrict__ dzb) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   const int r0 = blockIdx.y * 32;
   float s = 0.f;
-  if (c < 2 * D) {
+  if (c < NP * D) {
     const int r1 = min(G, r0 + 32);
-    for (int r = r0 + wid; r < r1; r += 4) s += part[(long)r * 2 * D + c];
+    for (int r = r0 + wid; r < r1; r += 4) s += part[(long)r * NP * D + c];
   }
   red[wid][lane] = s;
   __syncthreads();
-  if (wid == 0 && c < 2 * D) {
+  if (wid == 0 && c < NP * D) {
     const float v = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
     if (c < D) atomicAdd(dw + c, v);
-    else atomicAdd(db + c - D, v);
+    else if (c < 2 * D) atomicAdd(db + c - D, v);
+    else atomicAdd(dzb + c - 2 * D, v);
   }
 }
 
@@ -247,8 +280,8 @@ static int ln_bwd_resident() {
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)ln_bwd_kernel<NV>, 256,
-                                                       sizeof(float) * 8 * NV * 512);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)ln_bwd_kernel<NV, true>, 256,
+                                                       sizeof(float) * 12 * NV * 512);
     n = std::max(1, cus * std::max(1, per_cu));
   }
   return n;
@@ -277,14 +310,26 @@ void layernorm_fwd(const bf16_t* x, const bf16_t* w, const bf16_t* b, bf16_t* y,
 
 void layernorm_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const float* mean,
                    const float* rstd, const bf16_t* dres, bf16_t* dx, float* dw, float* db,
-                   float* workspace, int M, int D, hipStream_t stream) {
+                   float* workspace, int M, int D, hipStream_t stream, bf16_t* dz, float* dzb, float p,
+                   uint64_t seed) {
   const int grid = ln_bwd_grid(M, D);
-  const size_t smem = sizeof(float) * 8 * D;
-  MG_LN_DISPATCH(ln_bwd_kernel, dy, x, w, mean, rstd, dres, dx, workspace, M, D);
-  ln_colsum_kernel<<<dim3(cdiv(2 * D, 64), cdiv(grid, 32)), 256, 0, stream>>>(workspace, grid, D, dw, db);
+  const bool drop = dz != nullptr;
+  const int NP = drop ? 3 : 2;
+  const size_t smem = sizeof(float) * 4 * NP * D;
+  const uint32_t thr = drop ? dropout_threshold16(p) : 0u;
+  const LnDrop dr{dz, seed, graph_seed_ofs(), thr, dropout_scale16(thr)};
+#define MG_LN_BWD(NV)                                                                                   \
+  if (drop) ln_bwd_kernel<NV, true><<<grid, 256, smem, stream>>>(dy, x, w, mean, rstd, dres, dx, workspace, M, D, dr); \
+  else ln_bwd_kernel<NV, false><<<grid, 256, smem, stream>>>(dy, x, w, mean, rstd, dres, dx, workspace, M, D, dr);
+  if (D <= 512) { MG_LN_BWD(1) }
+  else if (D <= 1024) { MG_LN_BWD(2) }
+  else if (D <= 2048) { MG_LN_BWD(4) }
+  else { MG_LN_BWD(8) }
+#undef MG_LN_BWD
+  ln_colsum_kernel<<<dim3(cdiv(NP * D, 64), cdiv(grid, 32)), 256, 0, stream>>>(workspace, grid, D, NP, dw, db, dzb);
 }
 
-// floats of partial [dgamma | dbeta] rows layernorm_bwd needs
-size_t layernorm_bwd_workspace(int M, int D) { return (size_t)ln_bwd_grid(M, D) * 2 * D; }
+// floats of partial [dgamma | dbeta | dbias] rows layernorm_bwd needs
+size_t layernorm_bwd_workspace(int M, int D) { return (size_t)ln_bwd_grid(M, D) * 3 * D; }
 
 }  // namespace mg

@@ -71,13 +71,14 @@ class Block(nn.Module):
         self.mlp = MLP(config)
         self.config = config
 
-    def forward(self, x):
+    def forward(self, x, _links=None):
+        """``_links`` (GPU path, set by GPT.forward): (previous block's DropLink, this block's)."""
         if x.is_cuda:
-            return self._forward_gpu(x)
+            return self._forward_gpu(x, _links or (None, None))
         x = x + self.attn(self.ln_1(x))
         return x + self.mlp(self.ln_2(x))
 
-    def _forward_gpu(self, x):
+    def _forward_gpu(self, x, links=(None, None)):
         from ..ops.fused import TransformerBlockFn, _bf16
 
         B, T, D = x.shape
@@ -89,7 +90,7 @@ class Block(nn.Module):
               a.c_proj.bias, self.ln_2.weight, self.ln_2.bias, m.c_fc.weight, m.c_fc.bias,
               m.c_proj.weight, m.c_proj.bias]
         y = TransformerBlockFn.run(x.reshape(B * T, D), *[_bf16(p) for p in ps],
-                                     (B, T, c.n_head, p_attn, p_resid, c.layer_norm_eps))
+                                     (B, T, c.n_head, p_attn, p_resid, c.layer_norm_eps), links)
         return y.view(B, T, D)
 
 
@@ -181,7 +182,7 @@ class GPT(nn.Module):
         return logits, loss
 
     def _forward_gpu(self, idx, targets):
-        from ..ops.fused import EmbeddingFn, HeadFn, HeadLossFn, _bf16
+        from ..ops.fused import DropLink, EmbeddingFn, HeadFn, HeadLossFn, _bf16
 
         tr, c = self.transformer, self.config
         if not getattr(self, "_gpu_checked", False):
@@ -189,18 +190,24 @@ class GPT(nn.Module):
             self._gpu_checked = True
         p = c.embed_drop if self.training else 0.0
         x = EmbeddingFn.run(idx, _bf16(tr.wte.weight), _bf16(tr.wpe.weight), p)
+        # residual-dropout hand-offs: block l's MLP dropout backward runs inside the LayerNorm
+        # backward of its consumer (block l+1's ln_1, or ln_f) -- ops/fused.py DropLink
+        link = None
+        fuse = self.training and torch.is_grad_enabled() and c.resid_drop > 0
         for block in tr.h:
-            x = block(x)
+            out = DropLink(0.0, 0, _bf16(block.mlp.c_proj.bias)) if fuse else None
+            x = block(x, _links=(link, out))
+            link = out
         B, T, D = x.shape
         x2 = x.reshape(B * T, D)
         V = self.config.vocab_size
         if targets is not None:
             logits, loss = HeadLossFn.run(x2, _bf16(tr.ln_f.weight), _bf16(tr.ln_f.bias),
                                             _bf16(self.lm_head.weight), targets.reshape(-1).contiguous(),
-                                            c.layer_norm_eps)
+                                            c.layer_norm_eps, link)
             return logits.view(B, T, -1)[..., :V], loss
         logits = HeadFn.run(x2, _bf16(tr.ln_f.weight), _bf16(tr.ln_f.bias), _bf16(self.lm_head.weight),
-                              c.layer_norm_eps)
+                              c.layer_norm_eps, link)
         return logits.view(B, T, -1)[..., :V], None
 
     # -------------------------------------------------------------------------------- generation

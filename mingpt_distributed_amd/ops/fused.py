@@ -26,6 +26,41 @@ from ._ext import ext
 from .grads import before_use, finish, grad_target, note_use
 
 
+class DropLink:
+    """Hand-off of one residual-dropout backward between neighbouring fused ops.
+
+    Block l's MLP branch ends in ``x2 = x1 + dropout(c_proj(...))`` (/root/reference/mingpt/model.py:
+    188).  Its backward starts with dz = dropout'(dx2) plus the c_proj bias gradient, and dx2 is
+    the output of the LayerNorm backward of whatever consumed x2 (block l+1's ln_1 or the final
+    ln_f).  That consumer computes dz inside its LayerNorm-backward kernel (layernorm.hip DROP: one
+    read of the gradient instead of two) and leaves it here; block l's backward takes it instead of
+    running the separate dropout_bias_grad pass.  Created per forward by the producing block; a
+    consumer that never ran its backward leaves ``dz`` None and the producer falls back."""
+
+    __slots__ = ("p", "seed", "bias", "dz", "target")
+
+    def __init__(self, p: float, seed: int, bias: torch.Tensor):
+        self.p, self.seed, self.bias = p, seed, bias
+        self.dz = None
+        self.target = None
+
+    def ln_backward(self, C, dh, x, w, mean, rstd, dw, db, dres):
+        """The consumer's LayerNorm backward, with this link's dropout backward fused when it
+        applies: returns dx and leaves dz + the bias-gradient target for the producer."""
+        if self.p <= 0:
+            return C.layernorm_bwd(dh, x, w, mean, rstd, dw, db, dres)
+        self.target = grad_target(self.bias)
+        dx, self.dz = C.layernorm_bwd_dropout(dh, x, w, mean, rstd, dw, db, dres, self.target[0],
+                                              float(self.p), int(self.seed))
+        return dx
+
+
+def _ln_backward(C, link, dh, x, w, mean, rstd, dw, db, dres):
+    if link is None:
+        return C.layernorm_bwd(dh, x, w, mean, rstd, dw, db, dres)
+    return link.ln_backward(C, dh, x, w, mean, rstd, dw, db, dres)
+
+
 def new_seed() -> int:
     """Dropout seed from torch's CPU generator (reproducible under torch.manual_seed, no GPU sync)."""
     return int(torch.randint(1, 2 ** 62, (1,)).item())
@@ -104,7 +139,9 @@ class TransformerBlockFn(_EngineFn):
     """x [M, D] -> x + attn(ln1(x)) -> (+ mlp(ln2(.)))  with every op on a HIP kernel."""
 
     @staticmethod
-    def forward(ctx, x, ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, wfc, bfc, wp, bp, cfg):
+    def forward(ctx, x, ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, wfc, bfc, wp, bp, cfg, links=(None, None)):
+        """``links`` = (link_in, link_out): the previous block's MLP-dropout hand-off (computed by
+        this block's ln_1 backward) and this block's own (filled by the next consumer)."""
         B, T, H, p_attn, p_resid, eps = cfg
         C = ext()
         before_use(ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, wfc, bfc, wp, bp)
@@ -121,6 +158,10 @@ class TransformerBlockFn(_EngineFn):
         ctx.save_for_backward(x, h, mean1, rstd1, qkv, y, lse, amask, x1, h2, mean2, rstd2, gd, u)
         ctx.params = (ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, wfc, bfc, wp, bp)
         ctx.cfg, ctx.seeds = cfg, seeds
+        link_in, link_out = links
+        if link_out is not None:  # the MLP dropout this block's consumer will differentiate
+            link_out.p, link_out.seed, link_out.dz = p_resid, seeds[2], None
+        ctx.links = links
         return x2
 
     @staticmethod
@@ -133,8 +174,13 @@ class TransformerBlockFn(_EngineFn):
         g = {}
         for prm in ctx.params:
             g[id(prm)] = grad_target(prm)
+        link_in, link_out = ctx.links
         # ---- MLP: x2 = x1 + drop(gelu(h2 Wfc^T + bfc) Wp^T + bp)
-        if p_resid > 0:  # dz = dropout'(dx2) and d(bias) in one pass
+        if link_out is not None and link_out.dz is not None:
+            # dz = dropout'(dx2) and d(bias) came with dx2 (the consumer's LayerNorm backward)
+            dz, g[id(bp)] = link_out.dz, link_out.target
+            link_out.dz = link_out.target = None
+        elif p_resid > 0:  # dz = dropout'(dx2) and d(bias) in one pass
             dz = C.dropout_bias_grad(dx2, g[id(bp)][0], p_resid, ctx.seeds[2])
         else:
             dz = dx2
@@ -144,11 +190,13 @@ class TransformerBlockFn(_EngineFn):
         dpre = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=gd, dbias=g[id(bfc)][0])
         _wgrad(dpre, h2, g[id(wfc)])
         dh2 = _dgrad(dpre, wfc)
-        dx1 = C.layernorm_bwd(dh2, x1, ln2w, mean2, rstd2, g[id(ln2w)][0], g[id(ln2b)][0], dx2)
-        # ---- attention: x1 = x + drop(attn(h Wqkv^T + bqkv) Wo^T + bo)
+        # ---- attention: x1 = x + drop(attn(h Wqkv^T + bqkv) Wo^T + bo); the attention branch's
+        # dropout backward (dz) and bias gradient come out of ln_2's backward kernel
         if p_resid > 0:
-            dz = C.dropout_bias_grad(dx1, g[id(bo)][0], p_resid, ctx.seeds[1])
+            dx1, dz = C.layernorm_bwd_dropout(dh2, x1, ln2w, mean2, rstd2, g[id(ln2w)][0], g[id(ln2b)][0], dx2,
+                                              g[id(bo)][0], float(p_resid), int(ctx.seeds[1]))
         else:
+            dx1 = C.layernorm_bwd(dh2, x1, ln2w, mean2, rstd2, g[id(ln2w)][0], g[id(ln2b)][0], dx2)
             dz = dx1
             C.bias_grad(dz, g[id(bo)][0])
         _wgrad(dz, y, g[id(wo)])
@@ -158,9 +206,9 @@ class TransformerBlockFn(_EngineFn):
                                g[id(bqkv)][0])
         _wgrad(dqkv, h, g[id(wqkv)])
         dh = _dgrad(dqkv, wqkv)
-        dx = C.layernorm_bwd(dh, x, ln1w, mean1, rstd1, g[id(ln1w)][0], g[id(ln1b)][0], dx1)
+        dx = _ln_backward(C, link_in, dh, x, ln1w, mean1, rstd1, g[id(ln1w)][0], g[id(ln1b)][0], dx1)
         outs = [finish(prm, *g[id(prm)]) for prm in ctx.params]
-        return (dx, *outs, None)
+        return (dx, *outs, None, None)
 
 
 # ------------------------------------------------------------------------------------ head + loss
@@ -175,9 +223,10 @@ class HeadLossFn(_EngineFn):
     """loss = CE(LN_f(x) @ W^T, targets) with padded-vocab logits; returns (logits[M, Vpad], loss)."""
 
     @staticmethod
-    def forward(ctx, x, lnw, lnb, w, targets, eps):
+    def forward(ctx, x, lnw, lnb, w, targets, eps, link=None):
         C = ext()
         before_use(lnw, lnb, w)
+        ctx.link = link  # the last block's MLP-dropout hand-off (DropLink), or None
         V = w.shape[0]
         ld = (V + 127) // 128 * 128
         h, mean, rstd = C.layernorm_fwd(x, lnw, lnb, eps)
@@ -214,17 +263,18 @@ class HeadLossFn(_EngineFn):
         dh = G.gemm_dgrad(dlogits, w)  # W^T padded to the logits' row stride (zero columns)
         blw, mlw = grad_target(lnw)
         blb, mlb = grad_target(lnb)
-        dx = C.layernorm_bwd(dh, x, lnw, mean, rstd, blw, blb, None)
-        return dx, finish(lnw, blw, mlw), finish(lnb, blb, mlb), finish(w, bw, mw), None, None
+        dx = _ln_backward(C, ctx.link, dh, x, lnw, mean, rstd, blw, blb, None)
+        return dx, finish(lnw, blw, mlw), finish(lnb, blb, mlb), finish(w, bw, mw), None, None, None
 
 
 class HeadFn(_EngineFn):
     """logits = LN_f(x) @ W^T (inference / custom-loss path). Gradient flows to x and weights."""
 
     @staticmethod
-    def forward(ctx, x, lnw, lnb, w, eps):
+    def forward(ctx, x, lnw, lnb, w, eps, link=None):
         C = ext()
         before_use(lnw, lnb, w)
+        ctx.link = link
         V = w.shape[0]
         ld = (V + 7) // 8 * 8
         h, mean, rstd = C.layernorm_fwd(x, lnw, lnb, eps)
@@ -248,5 +298,5 @@ class HeadFn(_EngineFn):
         dh = G.gemm_nn(dl, w)
         blw, mlw = grad_target(lnw)
         blb, mlb = grad_target(lnb)
-        dx = C.layernorm_bwd(dh, x, lnw, mean, rstd, blw, blb, None)
-        return dx, finish(lnw, blw, mlw), finish(lnb, blb, mlb), finish(w, bw, mw), None
+        dx = _ln_backward(C, ctx.link, dh, x, lnw, mean, rstd, blw, blb, None)
+        return dx, finish(lnw, blw, mlw), finish(lnb, blb, mlb), finish(w, bw, mw), None, None
