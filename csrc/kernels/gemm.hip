@@ -661,9 +661,11 @@ MG_DEVICE void epilogue_direct(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
   const __amdgpu_buffer_rsrc_t ra = plane_rsrc(EPI == 2 ? args.aux : args.C, args.ldc, args.M, m0, n0);
   const uint32_t base = (uint32_t)(((long)(wm * CF::WTM + r) * args.ldc + colw + cpost) * 2);
   const uint32_t rstep = (uint32_t)(16 * args.ldc * 2);
-  float cs[EPI == 4 ? 4 * CF::FN : 1];  // EPI 4: this lane's column sums, [pair][8 columns]
+  // EPI 4: this lane's column sums, [pair][8 columns], padded to a power of two >= 16 for the fold
+  constexpr int NCS = EPI != 4 ? 1 : (4 * CF::FN <= 16 ? 16 : 4 * CF::FN <= 32 ? 32 : 64);
+  float cs[NCS];
 #pragma unroll
-  for (int k = 0; k < (EPI == 4 ? 4 * CF::FN : 1); ++k) cs[k] = 0.f;
+  for (int k = 0; k < NCS; ++k) cs[k] = 0.f;
   constexpr int NT_AUX = 2;  // non-temporal: the outputs are consumed by a later kernel
   // EPI 4 without preloaded side inputs: row group i + 1's GELU' pieces load while i is processed
   constexpr bool ROLL = (EPI == 3 || EPI == 4) && !PRE;
@@ -757,7 +759,7 @@ MG_DEVICE void epilogue_direct(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
       // (r, g) keeps sums 2 r, 2 r + 1 of its 4 FN values (pair r / 4, columns 2 (r % 4) + j); the
       // NWM row-waves meet in LDS (red_lds: a region no DMA writes at this point), then one atomic
       // per tile column
-      constexpr int NV = 4 * CF::FN;
+      constexpr int NV = NCS;
 #pragma unroll
       for (int M = 8; M >= 1; M >>= 1) {
         const bool hi = lane & M;
@@ -774,7 +776,7 @@ MG_DEVICE void epilogue_direct(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
 #pragma unroll
       for (int j = 0; j < NV / 16; ++j) {
         const int idx = (NV / 16) * r + j, jp = idx / 8, k = idx % 8;
-        red[wm * CF::BN + colw + 32 * jp + cpost + k] = cs[j];
+        if (jp < CF::FN / 2) red[wm * CF::BN + colw + 32 * jp + cpost + k] = cs[j];  // (padding: none)
       }
       __syncthreads();
       for (int c = threadIdx.x; c < CF::BN; c += CF::NT) {
@@ -1323,15 +1325,16 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
         }
       }
     }
-    // EPI 4's column-sum fold: B ring slot 2 (no prologue DMA lands there; the pieces past the last
-    // K-tile that may are older than the prologue's and are waited for first)
+    // EPI 4's column-sum fold: B ring slot 2 (of half-image 0 for m/n-contiguous B; no prologue DMA
+    // lands there; the pieces past the last K-tile that may are older than the prologue's and are
+    // waited for first)
     if constexpr (EPI == 4) {
       if (args.dbias) {
         if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (WK::PA + WK::PB)) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
-    epilogue_direct<CF, EPI, PRE>(args, acc, m0, n0, wm, wn, lane, sB + 2 * 16384, side);
+    epilogue_direct<CF, EPI, PRE>(args, acc, m0, n0, wm, wn, lane, sB + 2 * BS, side);
     if (!more) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA pieces past the last K-tile
       return;

@@ -8,7 +8,9 @@ SOS="tree $*"
 for so in $*; do
   n=$(basename $(dirname $so))
   MINGPT_EXT_SO=$so timeout -k 10 600 python -u -m pytest tests/test_gemm_gpu.py tests/test_bench_scale_gpu.py -q -x -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/tests_$n.log" 2>&1
-  s=$?; echo "$n tests: $(tail -1 $OUT/tests_$n.log)"; [ $s -eq 0 ] || exit $s
+  s=$?; echo "$n tests: $(tail -1 $OUT/tests_$n.log)"
+  # a crash / timeout ends the call; failed assertions are recorded and the timings still run
+  if [ $s -ne 0 ] && [ $s -ne 1 ]; then exit $s; fi
 done
 for rep in 1 2; do
   for so in $SOS; do
