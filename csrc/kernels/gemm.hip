@@ -41,17 +41,10 @@ using namespace mg;
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int BK = 64;
-#ifndef MG_GEMM_DIRECT_MAX
-#define MG_GEMM_DIRECT_MAX -1  // W4 bf16 epilogues EPI <= this on whole tiles: epilogue_direct (experiment)
-#endif
-#ifndef MG_W4_PERSIST
-#define MG_W4_PERSIST 0  // persistent W4 over tiles (needs the direct epilogue) (experiment)
-#endif
 #ifndef MG_GROUP_M
 #define MG_GROUP_M 8
 #endif
@@ -565,230 +558,6 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
   }
 }
 
-// ---- Direct epilogue (whole wave tiles, bf16 outputs): no LDS round trip.  The fragment layout
-// gives lane (row r = lane & 15, group g = lane >> 4) columns 16 j + 4 g .. +3 of fragment j; one
-// v_permlane16_swap per dword exchanges rows 1 / 3 of fragment j's registers with rows 0 / 2 of
-// fragment j+1's (guide T21 with 16-lane rows), after which the lane holds 8 consecutive columns:
-// fragment j + (g & 1), columns 8 (g >> 1) .. +7 -- one 16-byte store, and the four lanes of a row
-// cover 64 contiguous bytes per wave-instruction (16 rows x 64 B; the HBM access granule, unlike the
-// 32-byte row pieces of the fragment-direct stores measured in round 3).  fp32 values are swapped
-// (4 per pair) where a 16-byte side input must be applied before the bf16 rounding.
-MG_DEVICE uint32_t pl16_lo(uint32_t& x, uint32_t& y) {
-  const auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
-  x = r[0];
-  y = r[1];
-  return x;
-}
-MG_DEVICE void pl16(float& x, float& y) {
-  uint32_t a = __float_as_uint(x), b = __float_as_uint(y);
-  pl16_lo(a, b);
-  x = __uint_as_float(a);
-  y = __uint_as_float(b);
-}
-
-// Buffer descriptor of a [rows, ldc] bf16 plane from element (m0, n0) to the end of row M - 1:
-// rows >= M fall outside it, and so does a lane offset of kOOB (columns >= the output width), so
-// every store / load of the direct epilogue is issued unconditionally (exact vmcnt counts) and the
-// hardware drops / zero-fills the out-of-range ones.
-MG_DEVICE __amdgpu_buffer_rsrc_t plane_rsrc(const void* base, long ldc, int M, int m0, int n0) {
-  const uint64_t org = ((uint64_t)m0 * ldc + n0) * 2;
-  const uint64_t end = (uint64_t)M * ldc * 2;
-  const uint64_t left = end > org ? end - org : 0;
-  const uint64_t p = reinterpret_cast<uint64_t>(base) + org;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
-  const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)(left < 0xFFFFFF00ull ? left : 0xFFFFFF00ull));
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
-}
-
-// vector-memory instructions one wave issues in epilogue_direct after its side loads (stores only)
-template <class CF, int EPI>
-constexpr int direct_stores() { return CF::FM * (CF::FN / 2) * (EPI == 2 ? 2 : 1); }
-
-// side inputs of the whole tile in registers before the epilogue (128 VGPRs at FN = 8): the residual
-// always; GELU' only in the persistent kernel (there a side load waited for inside the epilogue would
-// also wait for the next tile's prologue DMA, issued before it); otherwise EPI 4 prefetches one row
-// group ahead (its column sums hold another 32 registers)
-template <int EPI, bool PERS>
-constexpr bool side_pre() { return EPI == 3 || (EPI == 4 && PERS); }
-template <class CF, int EPI, bool PRE>
-using DirectSide = uint4[CF::FM][PRE ? CF::FN / 2 : 1];
-
-// side: EPI 3 / 4 side input pieces of the whole wave tile, loaded by direct_side_loads (before the
-// next tile's prologue DMA in the persistent kernel, so waiting for them never waits for that DMA)
-template <class CF, int EPI, bool PRE>
-MG_DEVICE void direct_side_loads(const GemmArgs& args, int m0, int n0, int wm, int wn, int lane,
-                                 DirectSide<CF, EPI, PRE>& side) {
-  if constexpr (PRE) {
-    const int r = lane & 15, g = lane >> 4;
-    const int cpost = 16 * (g & 1) + 8 * (g >> 1);
-    const int nlim = args.N;
-    const int col = wn * CF::WTN + cpost;  // within the tile
-    const __amdgpu_buffer_rsrc_t rs = plane_rsrc(EPI == 3 ? (const void*)args.resid : (const void*)args.aux,
-                                                 args.ldc, args.M, m0, n0);
-    const uint32_t base = (uint32_t)(((long)(wm * CF::WTM + r) * args.ldc + col) * 2);
-    const uint32_t rstep = (uint32_t)(16 * args.ldc * 2);
-#pragma unroll
-    for (int i = 0; i < CF::FM; ++i)
-#pragma unroll
-      for (int jp = 0; jp < CF::FN / 2; ++jp) {
-        const uint32_t off = n0 + col + 32 * jp + 8 <= nlim ? base + i * rstep + 64 * jp : kOOB;
-        side[i][jp] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-      }
-  }
-}
-
-template <class CF, int EPI, bool PRE>
-MG_DEVICE void epilogue_direct(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int m0, int n0, int wm,
-                               int wn, int lane_in, char* red_lds, const DirectSide<CF, EPI, PRE>& side) {
-  static_assert(CF::FN % 2 == 0, "fragment pairs");
-  int lane = lane_in;
-  asm volatile("" : "+v"(lane));  // lane-derived addresses computed here, not hoisted into the K-loop
-  const int r = lane & 15, g = lane >> 4;
-  const int nlim = EPI == 0 ? (int)args.ldc : args.N;
-  const int cpost = 16 * (g & 1) + 8 * (g >> 1);  // post-swap column of fragment pair jp: 32 jp + cpost
-  const int colw = wn * CF::WTN;                   // wave tile's first column within the block tile
-  const int nb = n0 + colw + 4 * g;                // pre-swap columns of fragment j: nb + 16 j .. +3
-  uint2 bs[CF::FN];
-#pragma unroll
-  for (int j = 0; j < CF::FN; ++j) {
-    bs[j] = make_uint2(0u, 0u);
-    if constexpr (EPI == 1 || EPI == 2 || EPI == 3)
-      if (args.bias && nb + j * 16 < nlim) bs[j] = *reinterpret_cast<const uint2*>(args.bias + nb + j * 16);
-  }
-  const uint32_t dkey = EPI == 3 ? rowdrop_key(eff_seed(args.seed, args.sofs)) : 0u;
-  const __amdgpu_buffer_rsrc_t rc = plane_rsrc(args.C, args.ldc, args.M, m0, n0);
-  const __amdgpu_buffer_rsrc_t ra = plane_rsrc(EPI == 2 ? args.aux : args.C, args.ldc, args.M, m0, n0);
-  const uint32_t base = (uint32_t)(((long)(wm * CF::WTM + r) * args.ldc + colw + cpost) * 2);
-  const uint32_t rstep = (uint32_t)(16 * args.ldc * 2);
-  // EPI 4: this lane's column sums, [pair][8 columns], padded to a power of two >= 16 for the fold
-  constexpr int NCS = EPI != 4 ? 1 : (4 * CF::FN <= 16 ? 16 : 4 * CF::FN <= 32 ? 32 : 64);
-  float cs[NCS];
-#pragma unroll
-  for (int k = 0; k < NCS; ++k) cs[k] = 0.f;
-  constexpr int NT_AUX = 2;  // non-temporal: the outputs are consumed by a later kernel
-  // EPI 4 without preloaded side inputs: row group i + 1's GELU' pieces load while i is processed
-  constexpr bool ROLL = (EPI == 3 || EPI == 4) && !PRE;
-  uint4 sroll[2][ROLL ? CF::FN / 2 : 1];
-  const __amdgpu_buffer_rsrc_t rside = plane_rsrc(EPI == 3 ? (const void*)args.resid : (const void*)args.aux,
-                                                  args.ldc, args.M, m0, n0);
-  auto side_load = [&](int i, uint4 (&dst)[ROLL ? CF::FN / 2 : 1]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int jp = 0; jp < (ROLL ? CF::FN / 2 : 0); ++jp) {
-      const uint32_t off = n0 + colw + 32 * jp + cpost + 8 <= args.N ? base + i * rstep + 64 * jp : kOOB;
-      dst[jp] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rside, off, 0, 0));
-    }
-  };
-  if constexpr (ROLL) side_load(0, sroll[0]);
-#pragma unroll
-  for (int i = 0; i < CF::FM; ++i) {
-    const int m = m0 + wm * CF::WTM + 16 * i + r;
-    if constexpr (ROLL) {
-      if (i + 1 < CF::FM) side_load(i + 1, sroll[(i + 1) & 1]);
-    }
-#pragma unroll
-    for (int jp = 0; jp < CF::FN / 2; ++jp) {
-      const bool cok = n0 + colw + 32 * jp + cpost + 8 <= nlim;
-      const uint32_t off = cok ? base + i * rstep + 64 * jp : kOOB;
-      float v0[4], v1[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v0[e] = acc[i][2 * jp][e];
-        v1[e] = acc[i][2 * jp + 1][e];
-      }
-      if constexpr (EPI == 1 || EPI == 2 || EPI == 3) {
-        const uint2 b0 = bs[2 * jp], b1 = bs[2 * jp + 1];
-        v0[0] += bf2f(b0.x & 0xffffu); v0[1] += bf2f(b0.x >> 16); v0[2] += bf2f(b0.y & 0xffffu); v0[3] += bf2f(b0.y >> 16);
-        v1[0] += bf2f(b1.x & 0xffffu); v1[1] += bf2f(b1.x >> 16); v1[2] += bf2f(b1.y & 0xffffu); v1[3] += bf2f(b1.y >> 16);
-      }
-      if constexpr (EPI == 3 || EPI == 4) {
-        if constexpr (EPI == 3) {
-          if (args.thr) {
-            rowdrop4(v0, dkey, m, nb + 32 * jp, args.N, args.thr, args.scale);
-            rowdrop4(v1, dkey, m, nb + 32 * jp + 16, args.N, args.thr, args.scale);
-          }
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) pl16(v0[e], v1[e]);  // now v0 | v1 = 8 consecutive columns
-        uint4 sv;
-        if constexpr (ROLL) sv = sroll[i & 1][jp];
-        else sv = side[i][jp];
-        const uint32_t w[4] = {sv.x, sv.y, sv.z, sv.w};
-        float o[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float sk = bf2f((w[k >> 1] >> (16 * (k & 1))) & 0xffffu);
-          o[k] = EPI == 3 ? o[k] + sk : o[k] * sk;
-        }
-        if constexpr (EPI == 4) {  // bias gradient: fp32 column sums before the bf16 rounding
-          const bool ok = cok && m < args.M;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) cs[jp * 8 + k] += ok ? o[k] : 0.f;
-        }
-        const uint4 y = pack8(o);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, y), rc, off, 0, NT_AUX);
-      } else {
-        uint32_t gx0 = 0, gy0 = 0, gx1 = 0, gy1 = 0;
-        if constexpr (EPI == 2) {  // y = GELU(z) stored as C; GELU'(z) into aux
-          f32x2 ya, yb, ga0, gb0, yc, yd, gc0, gd0;
-          gelu2(f32x2{v0[0], v0[1]}, ya, ga0);
-          gelu2(f32x2{v0[2], v0[3]}, yb, gb0);
-          gelu2(f32x2{v1[0], v1[1]}, yc, gc0);
-          gelu2(f32x2{v1[2], v1[3]}, yd, gd0);
-          v0[0] = ya.x; v0[1] = ya.y; v0[2] = yb.x; v0[3] = yb.y;
-          v1[0] = yc.x; v1[1] = yc.y; v1[2] = yd.x; v1[3] = yd.y;
-          gx0 = pack2(ga0.x, ga0.y); gy0 = pack2(gb0.x, gb0.y);
-          gx1 = pack2(gc0.x, gc0.y); gy1 = pack2(gd0.x, gd0.y);
-        }
-        uint32_t x0 = pack2(v0[0], v0[1]), y0 = pack2(v0[2], v0[3]);
-        uint32_t x1 = pack2(v1[0], v1[1]), y1 = pack2(v1[2], v1[3]);
-        pl16_lo(x0, x1);
-        pl16_lo(y0, y1);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{x0, y0, x1, y1}, rc, off, 0, NT_AUX);
-        if constexpr (EPI == 2) {
-          pl16_lo(gx0, gx1);
-          pl16_lo(gy0, gy1);
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{gx0, gy0, gx1, gy1}, ra, off, 0, NT_AUX);
-        }
-      }
-    }
-  }
-  if constexpr (EPI == 4) {
-    if (args.dbias) {  // kernel argument: uniform over the workgroup
-      // the 16 lanes of a column group (lane bits 0-3 = rows) fold by transposing shuffles: lane
-      // (r, g) keeps sums 2 r, 2 r + 1 of its 4 FN values (pair r / 4, columns 2 (r % 4) + j); the
-      // NWM row-waves meet in LDS (red_lds: a region no DMA writes at this point), then one atomic
-      // per tile column
-      constexpr int NV = NCS;
-#pragma unroll
-      for (int M = 8; M >= 1; M >>= 1) {
-        const bool hi = lane & M;
-        const int C = NV * M / 8;  // values still held before this step
-#pragma unroll
-        for (int i2 = 0; i2 < C / 2; ++i2) {
-          const float send = hi ? cs[i2] : cs[i2 + C / 2];
-          const float keep = hi ? cs[i2 + C / 2] : cs[i2];
-          cs[i2] = keep + __shfl_xor(send, M, 64);
-        }
-      }
-      float* red = reinterpret_cast<float*>(red_lds);  // [NWM][BN]
-      __syncthreads();  // every wave's earlier use of this region is over
-#pragma unroll
-      for (int j = 0; j < NV / 16; ++j) {
-        const int idx = (NV / 16) * r + j, jp = idx / 8, k = idx % 8;
-        if (jp < CF::FN / 2) red[wm * CF::BN + colw + 32 * jp + cpost + k] = cs[j];  // (padding: none)
-      }
-      __syncthreads();
-      for (int c = threadIdx.x; c < CF::BN; c += CF::NT) {
-        float t = 0.f;
-#pragma unroll
-        for (int q = 0; q < CF::NWM; ++q) t += red[q * CF::BN + c];
-        if (n0 + c < args.N) atomicAdd(args.dbias + n0 + c, t);
-      }
-    }
-  }
-}
-
 // Shared epilogue: lane holds acc[i][j] = C[m0+wm*WTM+16i+(lane&15)][n0+wn*WTN+16j+4(lane>>4) .. +3].
 // LDSW: LDS bytes each wave may use for the staged form (the K-loop's buffers are free by then).
 template <class CF, int EPI, bool OUTF32, int LDSW>
@@ -1120,9 +889,8 @@ MG_DEVICE void mfma_acc_last(f32x4& acc, const bf16x8& a, const bf16x8& b) {
 }
 
 
-template <int BN, bool AK, bool BKC, int EPI, bool OUTF32, bool PERS>
+template <int BN, bool AK, bool BKC, int EPI, bool OUTF32>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
-  static_assert(!PERS || (!OUTF32 && EPI <= MG_GEMM_DIRECT_MAX), "persistent W4: direct bf16 epilogues only");
   static_assert(BN == 256 || BKC, "W4 with BN != 256 needs a k-contiguous B operand");
   using CF = Cfg<256, BN, 2, 2>;
   using WK = W4<BN>;
@@ -1132,25 +900,17 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
   const int wm = wid >> 1, wn = wid & 1;
 
   const int nblk = args.tiles_m * args.tiles_n * args.splits;
-  // launch-order index o -> (split, m0, n0): XCD-aware bijective remap (o & 7 = the XCD under
-  // round-robin placement), split slowest, then GROUP_M row tiles per column sweep.  The persistent
-  // form (PERS: one workgroup per CU looping over o = blockIdx.x + k * gridDim.x; gridDim.x is a
-  // multiple of 8, so a workgroup stays on its XCD) visits the tiles in the same order.
-  auto tile_of = [&](int o, int& sp, int& tm0, int& tn0) __attribute__((always_inline)) {
-    const int xcd = o & 7, q8 = nblk >> 3, r8 = nblk & 7;
-    const int wgs = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (o >> 3);
-    const int ntiles = args.tiles_m * args.tiles_n;
-    sp = wgs / ntiles;
-    const int wg = wgs % ntiles;
-    const int group = GROUP_M * args.tiles_n;
-    const int first_m = (wg / group) * GROUP_M;
-    const int gm = min(args.tiles_m - first_m, GROUP_M);
-    tm0 = (first_m + (wg % group) % gm) * 256;
-    tn0 = ((wg % group) / gm) * BN;
-  };
-  int orig = blockIdx.x;
-  int split, m0, n0;
-  tile_of(orig, split, m0, n0);
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int wgs = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int ntiles = args.tiles_m * args.tiles_n;
+  const int split = wgs / ntiles;
+  const int wg = wgs % ntiles;
+  const int group = GROUP_M * args.tiles_n;
+  const int first_m = (wg / group) * GROUP_M;
+  const int gm = min(args.tiles_m - first_m, GROUP_M);
+  const int m0 = (first_m + (wg % group) % gm) * 256;
+  const int n0 = ((wg % group) / gm) * BN;
 
 #ifdef MG_GEMM_STAMPS
   // diagnostic builds: [0..5] segments of K-tile MG_GEMM_STAMPS (phase A issue | wait | barrier |
@@ -1275,7 +1035,6 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
 
-  for (;;) {
   // slot pattern of K-tiles 6n .. 6n + 5: (A, B) = (0,0) (1,1) (0,2) (1,0) (0,1) (1,2)
   int kt = 0;
   for (; kt + 6 <= nk; kt += 6) {
@@ -1292,81 +1051,6 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
   if (kt + 3 < nk) ktile(kt + 3, I1{}, I0{});
   if (kt + 4 < nk) ktile(kt + 4, I0{}, I1{});
   W4_STAMP(8);
-  if constexpr (!OUTF32 && EPI <= MG_GEMM_DIRECT_MAX) {
-    // direct epilogue (no LDS staging): every tile, partial ones included (bounds by the buffer
-    // descriptors).  Side inputs first; then, in the persistent form, the next tile's prologue DMA
-    // (older than the epilogue's stores, so waiting for it never waits for them: the stores drain
-    // under the next tile's first K-tile)
-    constexpr bool PRE = side_pre<EPI, PERS>();
-    DirectSide<CF, EPI, PRE> side;
-    direct_side_loads<CF, EPI, PRE>(args, m0, n0, wm, wn, lane, side);
-    bool more = false;
-    int nm0 = m0, nn0 = n0;
-    if constexpr (PERS) {
-      const int nxt = orig + gridDim.x;
-      more = nxt < nblk;
-      if (more) {
-        int nsp;
-        tile_of(nxt, nsp, nm0, nn0);
-        orig = nxt;
-        // the ring is free: every wave's reads of the final K-tile ended before its last barrier
-        // (phase B only read the unused fragments of a K-tile past the end).  Short-lived stagers
-        // issue the prologue; the K-loop's own are re-initialised after the epilogue (their
-        // per-lane offsets live through it would cost the epilogue its registers)
-        Stager<AK, 256, 4, AHS> pa;
-        Stager<BKC, BN, 4, BHS> pb;
-        pa.init(args.A, args.a_bytes, args.lda, nm0, args.a_ext, kbeg, args.ka, kbeg + args.kchunk, wid, lane);
-        pb.init(args.B, args.b_bytes, args.ldb, nn0, args.b_ext, kbeg, args.kb, kbeg + args.kchunk, wid, lane);
-        pa.stage(smem, w4_tile(0, nk, tail_first));
-        pb.stage(sB, w4_tile(0, nk, tail_first));
-        if (nk > 1) {
-          pa.stage(smem + AS, w4_tile(1, nk, tail_first));
-          pb.stage(sB + BS, w4_tile(1, nk, tail_first));
-        }
-      }
-    }
-    // EPI 4's column-sum fold: B ring slot 2 (of half-image 0 for m/n-contiguous B; no prologue DMA
-    // lands there; the pieces past the last K-tile that may are older than the prologue's and are
-    // waited for first)
-    if constexpr (EPI == 4) {
-      if (args.dbias) {
-        if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (WK::PA + WK::PB)) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    epilogue_direct<CF, EPI, PRE>(args, acc, m0, n0, wm, wn, lane, sB + 2 * BS, side);
-    if (!more) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA pieces past the last K-tile
-      return;
-    }
-    m0 = nm0;
-    n0 = nn0;
-    {
-      int ln = lane;
-      asm volatile("" : "+v"(ln));  // recomputed, not kept alive across the epilogue
-      sta.init(args.A, args.a_bytes, args.lda, m0, args.a_ext, kbeg, args.ka, kbeg + args.kchunk, wid, ln);
-      stb.init(args.B, args.b_bytes, args.ldb, n0, args.b_ext, kbeg, args.kb, kbeg + args.kchunk, wid, ln);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // next tile's K-tile 0 landed (the epilogue's stores are younger and stay in flight)
-    constexpr int VW = WK::PA + WK::PB + direct_stores<CF, EPI>();  // vmcnt counts at most 63
-    if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VW < 63 ? VW : 63) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(direct_stores<CF, EPI>() < 63 ? direct_stores<CF, EPI>() : 63) : "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int j = 0; j < FN; ++j) fb0[j] = frag_k<BKC, 0, BHS>(sB, wn * FN + j, lane);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) fa0[i] = frag_k<AK, 0, AHS>(smem, wm * 8 + i, lane);
-    lds_ready(fa0);
-    lds_ready(fb0, false);
-    continue;
-  }
-  break;
-  }  // tile loop
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 #ifdef MG_GEMM_EPI_STAMPS
@@ -1384,17 +1068,6 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(const GemmArgs args) {
 #undef W4_KSTAMP
 }
 
-static int w4_cus() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    if (n < 8) n = 256;
-  }
-  return n;
-}
-
 template <int BN, bool AK, bool BKC, int EPI, bool OUTF32>
 void launch_w4(GemmArgs a, hipStream_t stream) {
   if constexpr (BN != 256 && !BKC) {
@@ -1406,16 +1079,14 @@ void launch_w4(GemmArgs a, hipStream_t stream) {
     a.kchunk = cdiv(a.K, BK) * BK;
     if (OUTF32) set_split(a, 256, 6);
     const int tiles = a.tiles_m * a.tiles_n * a.splits;
-    constexpr bool PERS = MG_W4_PERSIST && !OUTF32 && EPI <= MG_GEMM_DIRECT_MAX;
-    // persistent: one workgroup per CU (a multiple of 8: each keeps its XCD), looping over tiles
-    const int grid = PERS ? min(tiles, w4_cus() / 8 * 8) : tiles;
+    const int grid = tiles;
     static bool attr_set = false;
     if (!attr_set) {
-      hipFuncSetAttribute((const void*)gemm_w4_kernel<BN, AK, BKC, EPI, OUTF32, PERS>,
+      hipFuncSetAttribute((const void*)gemm_w4_kernel<BN, AK, BKC, EPI, OUTF32>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, W4<BN>::SMEM);
       attr_set = true;
     }
-    gemm_w4_kernel<BN, AK, BKC, EPI, OUTF32, PERS><<<grid, 256, W4<BN>::SMEM, stream>>>(a);
+    gemm_w4_kernel<BN, AK, BKC, EPI, OUTF32><<<grid, 256, W4<BN>::SMEM, stream>>>(a);
   }
 }
 
