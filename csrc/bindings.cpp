@@ -383,7 +383,8 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   CHECK_BF16(a); CHECK_BF16(b); CHECK_DEV(c);
   CHECK_CONTIG(a); CHECK_CONTIG(b); CHECK_CONTIG(c);
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm: 2-D operands required");
-  TORCH_CHECK(layout >= 0 && layout <= 2 && epi >= 0 && epi <= 4, "gemm: bad layout/epilogue");
+  TORCH_CHECK(layout >= 0 && layout <= 2 && epi >= 0 && epi <= 7 && epi != 5, "gemm: bad layout/epilogue");
+  TORCH_CHECK((epi != 6 || layout == 0) && (epi != 7 || layout == 1), "gemm: fragment-ordered GELU' epilogues: 6 NT, 7 NN");
   const int64_t lda = a.size(1), ldb = b.size(1), ldc = c.size(1);
   TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0, "gemm: row strides must be multiples of 8");
   TORCH_CHECK(M > 0 && N > 0 && M <= c.size(0) && N <= ldc, "gemm: output bounds");
@@ -395,7 +396,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     TORCH_CHECK(c.scalar_type() == at::kBFloat16, "gemm NT: bf16 output");
   } else if (layout == 1) {
     K = lda; ka = lda; kb = b.size(0); a_ext = a.size(0); b_ext = ldb;
-    TORCH_CHECK(kb <= K && M <= a_ext && N <= ldb && (epi == 0 || epi == 4), "gemm NN: shape mismatch");
+    TORCH_CHECK(kb <= K && M <= a_ext && N <= ldb && (epi == 0 || epi == 4 || epi == 7), "gemm NN: shape mismatch");
     TORCH_CHECK(c.scalar_type() == at::kBFloat16, "gemm NN: bf16 output");
   } else {
     K = a.size(0); ka = K; kb = b.size(0); a_ext = lda; b_ext = ldb;
@@ -410,10 +411,15 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
     bias_p = bp(*bias);
   }
   bf16_t* aux_p = nullptr;
-  if (epi == 2 || epi == 4) {
+  if (epi == 2 || epi == 4 || epi == 6 || epi == 7) {
     TORCH_CHECK(aux.has_value() && aux->defined(), "gemm: epilogue needs aux");
     CHECK_BF16(*aux); CHECK_CONTIG(*aux);
-    TORCH_CHECK(aux->numel() == c.numel(), "gemm: aux shape");
+    if (epi >= 6) {  // fragment order: whole 256 x 256 tiles
+      TORCH_CHECK(aux->numel() == ((M + 255) / 256) * ((N + 255) / 256) * 65536 && ldc == N,
+                  "gemm: fragment-ordered aux must hold ceil(M/256) * ceil(N/256) * 65536 elements");
+    } else {
+      TORCH_CHECK(aux->numel() == c.numel(), "gemm: aux shape");
+    }
     aux_p = bp(*aux);
   }
   const bf16_t* res_p = nullptr;
@@ -428,7 +434,7 @@ void gemm(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, int64_t
   float* dbias_p = nullptr;
   if (dbias.has_value() && dbias->defined()) {
     CHECK_F32(*dbias);
-    TORCH_CHECK(epi == 4 && dbias->numel() >= N, "gemm: dbias only with the gelu_bwd epilogue");
+    TORCH_CHECK((epi == 4 || epi == 7) && dbias->numel() >= N, "gemm: dbias only with the gelu_bwd epilogue");
     dbias_p = fp(*dbias);
   }
   DevGuard g(a.device());
@@ -463,7 +469,7 @@ at::Tensor attention_bwd(const at::Tensor& qkv, const at::Tensor& out, const at:
   CHECK_CONTIG(qkv); CHECK_CONTIG(out); CHECK_CONTIG(dout);
   const int64_t D3 = qkv.size(-1), D = D3 / 3, hd = D / H;
   TORCH_CHECK(qkv.numel() == B * T * D3 && out.numel() == B * T * D && dout.numel() == B * T * D &&
-              lse.numel() == B * H * T && hd % 8 == 0 && hd <= 128, "attention_bwd: shape mismatch");
+              lse.numel() == B * H * T && hd % 8 == 0 && hd <= 128 && D <= 4096, "attention_bwd: shape mismatch");
   TORCH_CHECK(B * T * H * 16 < (int64_t)1 << 31, "attention_bwd: B*T*H too large");
   DevGuard g(qkv.device());
   auto dqkv = at::empty_like(qkv);
@@ -692,6 +698,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("N"), py::arg("dbias") = py::none());
   m.def("gemm_set_variant", &mg::gemm_set_variant);
   m.def("gemm_get_variant", &mg::gemm_get_variant);
+  m.def("gemm_pick", &mg::gemm_pick, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("layout"));
   m.def("attention_set_bwd_mode", &mg::attention_set_bwd_mode);
   m.def("attention_fwd", &attention_fwd);
   m.def("attention_bwd", &attention_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"),

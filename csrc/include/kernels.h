@@ -88,7 +88,8 @@ void dropout_bias_grad(const bf16_t* dy, bf16_t* dx, float* db, long M, int N, f
                        hipStream_t stream);
 
 // gemm.hip -- layout 0 NT (fwd), 1 NN (dgrad), 2 TN (wgrad, fp32 accumulate)
-// epi: 0 none, 1 bias, 2 bias+gelu (gelu'(z) -> aux), 3 resid + dropout(acc + bias), 4 acc*gelu'(aux)
+// epi: 0 none, 1 bias, 2 bias+gelu (gelu'(z) -> aux), 3 resid + dropout(acc + bias), 4 acc*gelu'(aux);
+// 6 / 7: 2 / 4 with aux in the fragment order of the W4 256 x 256 tiles (gemm_frag_aux_elems)
 void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long lda, long ldb,
           long ldc, int M, int N, int K, int a_ext, int b_ext, int ka, int kb, const bf16_t* bias,
           bf16_t* aux, const bf16_t* resid, float p, uint64_t seed, hipStream_t stream,
@@ -97,6 +98,7 @@ void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long l
 void gemm_set_variant(int v);  // tile config override: 0 auto (per shape), 1 T128, 5 W4, 6 W4-192
 void gemm_set_debug_buffer(unsigned long long* p);  // MG_GEMM_STAMPS diagnostic builds
 int gemm_get_variant();
+int gemm_pick(int M, int N, int K, int layout);  // tile config the dispatcher picks (gemm_set_variant codes)
 
 // attention_train.hip / attention.hip -- causal flash attention; qkv [B*T, 3D], out [B*T, D],
 // lse [B*H*T]; dmask: dropout keep-bits generated by attention_fwd when p > 0

@@ -361,14 +361,16 @@ MG_DEVICE void staged_side_out(const GemmArgs& args, const char* st, const uint4
 #pragma unroll
     for (int u = 0; u < G; ++u) {
       float v[8] = {a[u].x, a[u].y, a[u].z, a[u].w, b[u].x, b[u].y, b[u].z, b[u].w};
-      const uint4 sv = sd[g0 + u];
-      const uint32_t w[4] = {sv.x, sv.y, sv.z, sv.w};
+      if constexpr (EPI != 7) {  // EPI 7: GELU' was applied in the fragment layout, before the staging
+        const uint4 sv = sd[g0 + u];
+        const uint32_t w[4] = {sv.x, sv.y, sv.z, sv.w};
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float s = bf2f((w[k >> 1] >> (16 * (k & 1))) & 0xffffu);
-        v[k] = EPI == 3 ? v[k] + s : v[k] * s;
+        for (int k = 0; k < 8; ++k) {
+          const float s = bf2f((w[k >> 1] >> (16 * (k & 1))) & 0xffffu);
+          v[k] = EPI == 3 ? v[k] + s : v[k] * s;
+        }
       }
-      if constexpr (EPI == 4 && staged_dbias<CF>()) {
+      if constexpr ((EPI == 4 || EPI == 7) && staged_dbias<CF>()) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) cs[k] += v[k];
       }
@@ -388,7 +390,7 @@ MG_DEVICE void staged_rows(const GemmArgs& args, const char* st, const uint4 (&s
     else staged_copy_out<EPI, S, CHF, PR, IT, false>(args, st, mr, nw, lane);
     return;
   }
-  if constexpr ((EPI == 3 || EPI == 4) && !CHECK && 64 % PR == 0 && IT % 2 == 0) {
+  if constexpr ((EPI == 3 || EPI == 4 || EPI == 7) && !CHECK && 64 % PR == 0 && IT % 2 == 0) {
     if (args.nt_out) staged_side_out<CF, EPI, S, PR, IT, true>(args, st, sd, mr, nw, lane, cs);
     else staged_side_out<CF, EPI, S, PR, IT, false>(args, st, sd, mr, nw, lane, cs);
     return;
@@ -407,10 +409,10 @@ MG_DEVICE void staged_rows(const GemmArgs& args, const char* st, const uint4 (&s
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float s = bf2f((w[k >> 1] >> (16 * (k & 1))) & 0xffffu);
-        v[k] = EPI == 3 ? v[k] + s : v[k] * s;
+        if constexpr (EPI != 7) v[k] = EPI == 3 ? v[k] + s : v[k] * s;
       }
       y = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7]));
-      if constexpr (EPI == 4 && staged_dbias<CF>()) {  // column sums (fp32, before the bf16 rounding)
+      if constexpr ((EPI == 4 || EPI == 7) && staged_dbias<CF>()) {  // column sums (fp32, before the bf16 rounding)
         if constexpr (CHECK) {
           const bool ok = m < args.M;
 #pragma unroll
@@ -450,7 +452,8 @@ template <class CF, int EPI, int LDSW>
 MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int m0, int n0,
                                int wm, int wn, int wid, int lane, char* smem,
                                unsigned long long* est = nullptr) {
-  constexpr bool F32 = EPI == 3 || EPI == 4;  // staged before a bf16 side input is applied
+  // EPI 6 / 7: EPI 2 / 4 with GELU' in the fragment order of the W4-256 tiles (frag_aux below)
+  constexpr bool F32 = EPI == 3 || EPI == 4 || EPI == 7;  // staged as fp32 (side input / column sums)
   constexpr int PL = EPI == 2 ? 2 : 1;           // planes: y (+ GELU' for EPI 2)
   constexpr int S = CF::WTN * (F32 ? 4 : 2) + 16;  // row stride: rows 4 banks apart (b64/b128 writes)
   constexpr int CHF = stage_chf(CF::FM, 16 * S * PL, LDSW);  // fragment rows per pass
@@ -467,10 +470,17 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
 #pragma unroll
   for (int j = 0; j < CF::FN; ++j) {
     bs[j] = make_uint2(0u, 0u);
-    if constexpr (EPI == 1 || EPI == 2 || EPI == 3)
+    if constexpr (EPI == 1 || EPI == 2 || EPI == 3 || EPI == 6)
       if (args.bias && nb + j * 16 < nlim) bs[j] = *reinterpret_cast<const uint2*>(args.bias + nb + j * 16);
   }
   const bf16_t* __restrict__ side = EPI == 3 ? args.resid : args.aux;
+  // fragment-ordered GELU' plane (EPI 6 writes, EPI 7 reads): per 256 x 256 tile 65536 elements in
+  // (wave, i, j, lane, 4) order, so each fragment is one fully contiguous 512-byte wave-instruction
+  // from the registers (no LDS staging for that plane) and the fc2 data gradient (same W4-256 tile
+  // grid and fragment layout) reads exactly the values its lanes need before its own staging
+  bf16_t* const frag_aux = (EPI == 6 || EPI == 7)
+      ? args.aux + ((long)(m0 / 256) * args.tiles_n + n0 / 256) * 65536 + (long)wid * CF::FM * CF::FN * 256 + lane * 4
+      : nullptr;
   const uint32_t dkey = EPI == 3 ? rowdrop_key(eff_seed(args.seed, args.sofs)) : 0u;  // dropout key
   const bool full = nw + CF::WTN <= nlim && mw + CF::WTM <= args.M;  // wave-uniform: no per-piece checks
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // EPI 4 + dbias: this lane's column sums
@@ -478,7 +488,15 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
   for (int c = 0; c < CF::FM / CHF; ++c) {
     // side inputs of this pass first: their latency hides under the LDS staging
     uint4 sd[F32 ? IT : 1];
-    if constexpr (F32) {
+    uint2 fx[EPI == 7 ? CHF : 1][EPI == 7 ? CF::FN : 1];
+    if constexpr (EPI == 7) {  // this pass's GELU' fragments: contiguous 512-byte loads
+#pragma unroll
+      for (int ii = 0; ii < CHF; ++ii)
+#pragma unroll
+        for (int j = 0; j < CF::FN; ++j)
+          fx[ii][j] = *reinterpret_cast<const uint2*>(frag_aux + ((c * CHF + ii) * CF::FN + j) * 256);
+    }
+    if constexpr (EPI == 3 || EPI == 4) {
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
         const int e = it * 64 + lane, r = e / PR, n = nw + (e % PR) * 8;
@@ -497,11 +515,25 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
       for (int j = 0; j < CF::FN; ++j) {
         const int n = nb + j * 16;
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        if constexpr (EPI == 1 || EPI == 2 || EPI == 3) {
+        if constexpr (EPI == 1 || EPI == 2 || EPI == 3 || EPI == 6) {
           v[0] += bf2f(bs[j].x & 0xffffu); v[1] += bf2f(bs[j].x >> 16);
           v[2] += bf2f(bs[j].y & 0xffffu); v[3] += bf2f(bs[j].y >> 16);
         }
         const int col = j * 16 + (lane >> 4) * 4;
+        if constexpr (EPI == 6) {  // y = GELU(z) staged; GELU'(z) straight to its fragment-ordered plane
+          f32x2 y0, y1, g0, g1;
+          gelu2(f32x2{v[0], v[1]}, y0, g0);
+          gelu2(f32x2{v[2], v[3]}, y1, g1);
+          v[0] = y0.x; v[1] = y0.y; v[2] = y1.x; v[3] = y1.y;
+          typedef unsigned v2u __attribute__((ext_vector_type(2)));
+          __builtin_nontemporal_store(v2u{pack2(g0.x, g0.y), pack2(g1.x, g1.y)},
+                                      reinterpret_cast<v2u*>(frag_aux + (i * CF::FN + j) * 256));
+        }
+        if constexpr (EPI == 7) {  // x GELU'(z) in the fragment layout (fp32 product, as EPI 4)
+          const uint2 gx = fx[ii][j];
+          v[0] *= bf2f(gx.x & 0xffffu); v[1] *= bf2f(gx.x >> 16);
+          v[2] *= bf2f(gx.y & 0xffffu); v[3] *= bf2f(gx.y >> 16);
+        }
         if constexpr (EPI == 2) {  // y = GELU(z); GELU'(z) into the second plane (packed fp32 math)
           f32x2 y0, y1, g0, g1;
           gelu2(f32x2{v[0], v[1]}, y0, g0);
@@ -533,7 +565,7 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
     if (est) est[2] = __builtin_amdgcn_s_memtime();  // staged reads + global stores issued
 #endif
   }
-  if constexpr (EPI == 4 && staged_dbias<CF>()) {
+  if constexpr ((EPI == 4 || EPI == 7) && staged_dbias<CF>()) {
     if (args.dbias) {  // kernel argument: uniform over the workgroup
       // lanes sharing a piece index (lane % PR) fold by shuffles, the NWM row-waves through LDS,
       // then one atomic per tile column with 64 contiguous floats per wave-instruction
@@ -564,7 +596,7 @@ template <class CF, int EPI, bool OUTF32, int LDSW>
 MG_DEVICE void epilogue(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int m0, int n0, int wm,
                         int wn, int wid, int lane, char* smem, unsigned long long* est = nullptr) {
   if constexpr (!OUTF32) {
-    if (EPI != 4 || !args.dbias || staged_dbias<CF>()) {
+    if ((EPI != 4 && EPI != 7) || !args.dbias || staged_dbias<CF>()) {
       epilogue_staged<CF, EPI, LDSW>(args, acc, m0, n0, wm, wn, wid, lane, smem, est);
       return;
     }
@@ -1162,6 +1194,8 @@ void dispatch(const GemmArgs& a, hipStream_t stream) {
 
 namespace mg {
 
+int gemm_pick(int M, int N, int K, int layout) { return pick_config(M, N, K, layout); }
+
 void gemm_set_variant(int v) {
   if (v != 0 && v != 1 && v != 5 && v != 6) throw std::invalid_argument("gemm_set_variant: 0 (auto), 1 (T128), 5 (W4), 6 (W4 BN=192)");
   g_variant = v;
@@ -1195,9 +1229,11 @@ void gemm(int layout, int epi, const bf16_t* A, const bf16_t* B, void* C, long l
     else if (epi == 1) dispatch<true, true, 1, false>(a, stream);
     else if (epi == 2) dispatch<true, true, 2, false>(a, stream);
     else if (epi == 3) dispatch<true, true, 3, false>(a, stream);
+    else if (epi == 6) launch_w4<256, true, true, 6, false>(a, stream);  // fragment-ordered GELU': W4-256 only
     else dispatch<true, true, 4, false>(a, stream);  // dgrad as NT against a transposed weight
   } else if (layout == 1) {
     if (epi == 4) dispatch<true, false, 4, false>(a, stream);
+    else if (epi == 7) launch_w4<256, true, false, 7, false>(a, stream);
     else dispatch<true, false, 0, false>(a, stream);
   } else {
     dispatch<false, false, 0, true>(a, stream);

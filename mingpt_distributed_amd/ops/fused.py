@@ -152,12 +152,16 @@ class TransformerBlockFn(_EngineFn):
         y, lse, amask = C.attention_fwd(qkv, B, T, H, float(p_attn), seeds[0])
         x1 = G.gemm_nt(y, wo, bias=bo, epi="resid", resid=x, p=p_resid, seed=seeds[1])
         h2, mean2, rstd2 = C.layernorm_fwd(x1, ln2w, ln2b, eps)
-        gd = torch.empty((x.shape[0], wfc.shape[0]), dtype=torch.bfloat16, device=x.device)  # GELU'(z)
-        u = G.gemm_nt(h2, wfc, bias=bfc, epi="gelu", pre_out=gd)
+        # GELU'(z) for the fc2 data gradient: in the fragment order of the W4 tiles when both GEMMs
+        # run on them (no LDS staging for that plane in either epilogue), else row-major
+        M, N4 = x.shape[0], wfc.shape[0]
+        frag = G.frag_aux_ok(M, N4, x.shape[1])
+        gd = torch.empty(G.frag_aux_elems(M, N4) if frag else (M, N4), dtype=torch.bfloat16, device=x.device)
+        u = G.gemm_nt(h2, wfc, bias=bfc, epi="gelu", pre_out=gd, frag=frag)
         x2 = G.gemm_nt(u, wp, bias=bp, epi="resid", resid=x1, p=p_resid, seed=seeds[2])
         ctx.save_for_backward(x, h, mean1, rstd1, qkv, y, lse, amask, x1, h2, mean2, rstd2, gd, u)
         ctx.params = (ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, wfc, bfc, wp, bp)
-        ctx.cfg, ctx.seeds = cfg, seeds
+        ctx.cfg, ctx.seeds, ctx.frag = cfg, seeds, frag
         link_in, link_out = links
         if link_out is not None:  # the MLP dropout this block's consumer will differentiate
             link_out.p, link_out.seed, link_out.dz = p_resid, seeds[2], None
@@ -187,7 +191,7 @@ class TransformerBlockFn(_EngineFn):
             C.bias_grad(dz, g[id(bp)][0])
         _wgrad(dz, u, g[id(wp)])
         # fc bias gradient: column sums of dpre in the GELU' epilogue
-        dpre = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=gd, dbias=g[id(bfc)][0])
+        dpre = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=gd, dbias=g[id(bfc)][0], aux_frag=ctx.frag)
         _wgrad(dpre, h2, g[id(wfc)])
         dh2 = _dgrad(dpre, wfc)
         # ---- attention: x1 = x + drop(attn(h Wqkv^T + bqkv) Wo^T + bo); the attention branch's

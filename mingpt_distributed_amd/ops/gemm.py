@@ -22,6 +22,21 @@ import torch
 from ._ext import ext
 
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_RESID, EPI_GELU_BWD = 0, 1, 2, 3, 4
+EPI_GELU_FRAG, EPI_GELU_BWD_FRAG = 6, 7  # GELU' plane in the fragment order of the W4 256x256 tiles
+
+
+def frag_aux_elems(M: int, N: int) -> int:
+    """Elements of a fragment-ordered GELU' plane for an [M, N] output (whole 256x256 tiles)."""
+    return -(-M // 256) * -(-N // 256) * 65536
+
+
+def frag_aux_ok(M: int, N: int, K: int) -> bool:
+    """The fragment-ordered GELU' plane (epilogues 6 / 7) needs producer and consumer on the same
+    256x256 tile grid: true when the dispatcher would pick W4-256 for both the forward [M, N, K]
+    and the data gradient [M, N, K'] anyway (every GPT-2 / gpt2-xl training shape), so forcing
+    them costs nothing."""
+    C = ext()
+    return C.gemm_get_variant() == 0 and C.gemm_pick(M, N, K, 0) == 5 and C.gemm_pick(M, N, K, 1) == 5
 
 
 # Row-chunked launches are no longer needed for operands past 4 GiB (the GPT-2 logits beyond ~42k
@@ -50,10 +65,13 @@ def _check2d(t, name):
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: Optional[torch.Tensor] = None,
             epi: str = "none", resid: Optional[torch.Tensor] = None, p: float = 0.0, seed: int = 0,
             pre_out: Optional[torch.Tensor] = None, ld: Optional[int] = None,
-            aux: Optional[torch.Tensor] = None, dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
+            aux: Optional[torch.Tensor] = None, dbias: Optional[torch.Tensor] = None,
+            frag: bool = False) -> torch.Tensor:
     """C = A @ B^T with a fused epilogue. ``ld`` pads the output row stride (logits).
     ``gelu`` writes GELU'(z) into ``pre_out``; ``gelu_bwd`` multiplies by ``aux`` (that GELU') and,
-    with ``dbias`` (fp32 [N]), also adds the output's column sums into it (the bias gradient)."""
+    with ``dbias`` (fp32 [N]), also adds the output's column sums into it (the bias gradient).
+    ``frag=True`` (``gelu`` only): ``pre_out`` is a fragment-ordered plane of
+    ``frag_aux_elems(M, N)`` elements for ``gemm_nn(..., aux_frag=True)``."""
     _check2d(a, "A")
     _check2d(b, "B")
     M, K = a.shape
@@ -64,8 +82,14 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: Optional[torch.Tensor] = 
             "gelu_bwd": EPI_GELU_BWD}[epi]
     if code == EPI_BIAS and bias is None:
         code = EPI_NONE
+    if frag:
+        if code != EPI_GELU:
+            raise ValueError("gemm_nt: frag=True is the gelu epilogue's fragment-ordered GELU' plane")
+        code = EPI_GELU_FRAG
     side = aux if code == EPI_GELU_BWD else pre_out
     chunks = _row_chunks(M, 2 * K, 2 * ld)
+    if len(chunks) > 1 and code == EPI_GELU_FRAG:
+        raise ValueError("gemm_nt: the fragment-ordered GELU' plane is one launch; operand too large")
     if len(chunks) > 1 and code == EPI_RESID and p > 0:
         raise ValueError("gemm_nt: residual dropout keys its mask on the global row; operand too large")
     for r0, r1 in chunks:
@@ -83,23 +107,25 @@ def transpose(w: torch.Tensor, ld: Optional[int] = None) -> torch.Tensor:
 
 def gemm_dgrad(dy: torch.Tensor, w: torch.Tensor, *, epi: str = "none",
                aux: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None,
-               dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
+               dbias: Optional[torch.Tensor] = None, aux_frag: bool = False) -> torch.Tensor:
     """dX = dY @ W (W [N_out, N_in] as stored by nn.Linear).  Block shapes run NN straight from the
     stored weight (the W4 kernel's transposing LDS reads; no per-step transposed copy:
     bench/dgrad_nn_vs_nt.py); a long reduction (the LM head's K = vocab) runs NT against W^T, where
     the 128x96-wave W4 tile applies.  With ``epi="gelu_bwd"`` and ``dbias`` (fp32 [N_in]), the
     column sums of the result (the next bias gradient) are accumulated in the epilogue."""
-    if wt is None and dy.shape[1] < 8192 and w.shape[0] == dy.shape[1]:
-        return gemm_nn(dy, w, epi=epi, aux=aux, dbias=dbias)
+    if aux_frag or (wt is None and dy.shape[1] < 8192 and w.shape[0] == dy.shape[1]):
+        return gemm_nn(dy, w, epi=epi, aux=aux, dbias=dbias, aux_frag=aux_frag)
     if wt is None:
         wt = transpose(w, dy.shape[1])
     return gemm_nt(dy, wt, epi=epi, aux=aux, dbias=dbias)
 
 
 def gemm_nn(a: torch.Tensor, b: torch.Tensor, *, epi: str = "none",
-            aux: Optional[torch.Tensor] = None, dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
+            aux: Optional[torch.Tensor] = None, dbias: Optional[torch.Tensor] = None,
+            aux_frag: bool = False) -> torch.Tensor:
     """C = A @ B (B row-major [K, N]); ``gelu_bwd`` multiplies by ``aux`` (a stored GELU') and,
-    with ``dbias`` (fp32 [N]), adds the column sums of the fp32 C into it (staged epilogue)."""
+    with ``dbias`` (fp32 [N]), adds the column sums of the fp32 C into it (staged epilogue).
+    ``aux_frag``: ``aux`` is the fragment-ordered plane of ``gemm_nt(..., frag=True)``."""
     _check2d(a, "A")
     _check2d(b, "B")
     M, K = a.shape
@@ -108,6 +134,11 @@ def gemm_nn(a: torch.Tensor, b: torch.Tensor, *, epi: str = "none",
     code = {"none": EPI_NONE, "gelu_bwd": EPI_GELU_BWD}[epi]
     if dbias is not None and code != EPI_GELU_BWD:
         raise ValueError("gemm_nn: dbias is fused only into the gelu_bwd epilogue")
+    if aux_frag:
+        if code != EPI_GELU_BWD:
+            raise ValueError("gemm_nn: aux_frag is the gelu_bwd epilogue's fragment-ordered GELU' plane")
+        ext().gemm(a, b, c, 1, EPI_GELU_BWD_FRAG, None, aux, None, 0.0, 0, M, N, dbias)
+        return c
     chunks = _row_chunks(M, 2 * K, 2 * N)
     for r0, r1 in chunks:
         sl = (lambda t: t if t is None or len(chunks) == 1 else t[r0:r1])

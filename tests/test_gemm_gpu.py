@@ -209,3 +209,32 @@ def test_deleted_tile_configs_are_rejected(tile_config):
         with pytest.raises(Exception):
             ext().gemm_set_variant(v)
     ext().gemm_set_variant(tile_config)
+
+
+@pytest.mark.parametrize("M", [8192, 1000])
+def test_fragment_ordered_gelu_plane(M, tile_config):
+    """Epilogues 6 / 7: the fc forward writes GELU'(z) in the fragment order of the W4 256x256 tiles
+    (no LDS staging for that plane) and the fc2 data gradient reads it in the same order.  y, the
+    data gradient and its bias-gradient column sums equal the row-major epilogues 2 / 4 exactly
+    (same products, same staging of the other plane); partial tiles (M = 1000) included."""
+    Nin, Nout = 768, 3072
+    x, w, b = _bf(M, Nin, seed=41), _bf(Nout, Nin, seed=42, scale=0.05), _bf(Nout, seed=43, scale=0.1)
+    dz, wp = _bf(M, Nin, seed=44), _bf(Nin, Nout, seed=45, scale=0.05)
+    pre = torch.empty(M, Nout, device=DEV, dtype=torch.bfloat16)
+    y0 = G.gemm_nt(x, w, bias=b, epi="gelu", pre_out=pre)
+    fr = torch.empty(G.frag_aux_elems(M, Nout), device=DEV, dtype=torch.bfloat16)
+    y1 = G.gemm_nt(x, w, bias=b, epi="gelu", pre_out=fr, frag=True)
+    if tile_config in (0, 5):  # the same W4-256 kernel on both sides: bitwise
+        assert torch.equal(y1, y0)
+    else:
+        torch.testing.assert_close(y1, y0, atol=2e-2, rtol=2e-2)
+    db0 = torch.zeros(Nout, device=DEV)
+    db1 = torch.zeros(Nout, device=DEV)
+    d0 = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=pre, dbias=db0)
+    d1 = G.gemm_dgrad(dz, wp, epi="gelu_bwd", aux=fr, dbias=db1, aux_frag=True)
+    if tile_config in (0, 5):  # the same W4-256 kernel on both sides: bitwise
+        assert torch.equal(d1, d0)
+    ref = (dz.float() @ wp.float()) * pre.float()
+    _check(d1, ref, Nin)
+    tol = 6e-3 * d1.float().pow(2).sum(0).max().item() ** 0.5 + 1e-2
+    torch.testing.assert_close(db1, d1.float().sum(0), atol=tol, rtol=1e-3)
