@@ -581,81 +581,36 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
   }
 }
 
-// partial mode: dqkv Q slot = bf16(scale * sum of the dQ partials of key blocks kb <= t / KB), and
-// (dbias != null) the fp32 column sums of the Q gradient -- the Q third of the qkv bias gradient,
-// which used to be a separate bias_grad pass re-reading dQ (50 us per GPT-2 layer at B = 128).
-// Block = C8 = D / 8 chunk lanes x RS row groups over a contiguous strip of rows (grid: a few
-// blocks per CU), each lane summing its 8 columns over the strip; the row groups fold through LDS
-// and each block adds its D column sums with one atomic each.  Two rows per iteration keep up to
-// 16 16-byte partial loads in flight per lane.
-__global__ __launch_bounds__(512) void attn_dq_finalize_kernel(const float* __restrict__ dq,
+// partial mode: dqkv Q slot = bf16(scale * sum of the dQ partials of key blocks kb <= t / KB)
+__global__ __launch_bounds__(256) void attn_dq_finalize_kernel(const float* __restrict__ dq,
                                                                bf16_t* __restrict__ dqkv, int rows,
-                                                               int D, int T, int KB, long part, float sc,
-                                                               float* __restrict__ dbias) {
-  __shared__ float red[512 * 8];
-  const int C8 = D / 8, RS = blockDim.x / C8;
-  const int t = threadIdx.x, ch = t % C8, rs = t / C8;
-  const int c = ch * 8;
-  const int per = (rows + gridDim.x - 1) / gridDim.x;
-  const int r0 = blockIdx.x * per, r1 = min(rows, r0 + per);
-  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  auto load_row = [&](int r, float4 (&y)[4][2], int& np) __attribute__((always_inline)) {
-    np = (r % T) / KB + 1;
-    const float* src = dq + (long)r * D + c;
+                                                               int D, int T, int KB, long part, float sc) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;  // over rows * D/8
+  const int d8 = D / 8;
+  if (i >= (long)rows * d8) return;
+  const int r = (int)(i / d8);  // 32-bit operands: a cheap division
+  const int c = (int)(i - (long)r * d8) * 8;
+  const int np = (r % T) / KB + 1;
+  const float* src = dq + (long)r * D + c;
+  float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
+  for (int k = 0; k < np; k += 4) {  // four partials' loads in flight before the adds
+    float4 y[4][2];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {  // partials are read once: non-temporal
-      const bool ok = u < np;
-      const float* s = src + (long)(ok ? u : 0) * part;
+      const bool ok = k + u < np;
+      const float* s = src + (long)(ok ? k + u : k) * part;
       const uint4 a0 = ok ? ld16_nt(s) : make_uint4(0, 0, 0, 0), a1 = ok ? ld16_nt(s + 4) : make_uint4(0, 0, 0, 0);
       y[u][0] = make_float4(__uint_as_float(a0.x), __uint_as_float(a0.y), __uint_as_float(a0.z), __uint_as_float(a0.w));
       y[u][1] = make_float4(__uint_as_float(a1.x), __uint_as_float(a1.y), __uint_as_float(a1.z), __uint_as_float(a1.w));
     }
-  };
-  auto finish_row = [&](int r, const float4 (&y)[4][2], int np) __attribute__((always_inline)) {
-    float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       x0.x += y[u][0].x; x0.y += y[u][0].y; x0.z += y[u][0].z; x0.w += y[u][0].w;
       x1.x += y[u][1].x; x1.y += y[u][1].y; x1.z += y[u][1].z; x1.w += y[u][1].w;
     }
-    const float* src = dq + (long)r * D + c;
-    for (int k = 4; k < np; ++k) {  // T > 4 KB only
-      const float4 a = *reinterpret_cast<const float4*>(src + (long)k * part);
-      const float4 b = *reinterpret_cast<const float4*>(src + (long)k * part + 4);
-      x0.x += a.x; x0.y += a.y; x0.z += a.z; x0.w += a.w;
-      x1.x += b.x; x1.y += b.y; x1.z += b.z; x1.w += b.w;
-    }
-    const float f[8] = {x0.x * sc, x0.y * sc, x0.z * sc, x0.w * sc, x1.x * sc, x1.y * sc, x1.z * sc, x1.w * sc};
-    st16_nt(dqkv + (long)r * 3L * D + c, pack8(f));
-#pragma unroll
-    for (int j = 0; j < 8; ++j) cs[j] += f[j];
-  };
-  if (rs < RS) {
-    int r = r0 + rs;
-    for (; r + RS < r1; r += 2 * RS) {
-      float4 ya[4][2], yb[4][2];
-      int na, nb;
-      load_row(r, ya, na);
-      load_row(r + RS, yb, nb);
-      finish_row(r, ya, na);
-      finish_row(r + RS, yb, nb);
-    }
-    if (r < r1) {
-      float4 ya[4][2];
-      int na;
-      load_row(r, ya, na);
-      finish_row(r, ya, na);
-    }
   }
-  if (!dbias) return;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) red[t * 8 + j] = rs < RS ? cs[j] : 0.f;
-  __syncthreads();
-  for (int k = t; k < D; k += blockDim.x) {  // column k = chunk k / 8, element k % 8
-    float s = 0.f;
-    for (int g = 0; g < RS; ++g) s += red[((g * C8) + k / 8) * 8 + k % 8];
-    atomicAdd(dbias + k, s);
-  }
+  const float f[8] = {x0.x * sc, x0.y * sc, x0.z * sc, x0.w * sc, x1.x * sc, x1.y * sc, x1.z * sc, x1.w * sc};
+  st16_nt(dqkv + (long)r * 3L * D + c, pack8(f));
 }
 
 template <int NKS, int KW, bool PERSIST>
@@ -757,13 +712,12 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
     default: launch_bwd<8, 4>(a, stream); break;
   }
   if (!persistent) {
-    // the Q columns' bias gradient summed by the finalize (the K / V ones by the key-block kernel)
-    const int c8 = D / 8, rs = c8 >= 256 ? 1 : 256 / c8;  // D <= 4096 (c8 <= 512: the block)
-    const int grid = std::max(1, std::min(cdiv((long)B * T, 16 * rs), 4 * num_cus()));
-    attn_dq_finalize_kernel<<<grid, c8 * rs, 0, stream>>>(dq, dqkv, B * T, D, T, bwd_keys_per_block(hd), a.dq_part,
-                                                          0.6931471805599453f * a.dscale, fuse_db ? dbias : nullptr);
+    const long n8 = (long)B * T * (H * hd / 8);
+    attn_dq_finalize_kernel<<<(unsigned)cdiv(n8, 256), 256, 0, stream>>>(
+        dq, dqkv, B * T, H * hd, T, bwd_keys_per_block(hd), a.dq_part, 0.6931471805599453f * a.dscale);
   }
-  if (dbias && !fuse_db) bias_grad(dqkv, dbias, (long)B * T, 3 * D, stream);
+  if (fuse_db) bias_grad(dqkv, dbias, (long)B * T, D, stream, 3L * D);  // Q columns
+  else if (dbias) bias_grad(dqkv, dbias, (long)B * T, 3 * D, stream);
 }
 
 void attention_set_bwd_mode(int mode) { g_bwd_mode = mode; }

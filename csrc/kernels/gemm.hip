@@ -390,7 +390,7 @@ MG_DEVICE void staged_rows(const GemmArgs& args, const char* st, const uint4 (&s
     else staged_copy_out<EPI, S, CHF, PR, IT, false>(args, st, mr, nw, lane);
     return;
   }
-  if constexpr ((EPI == 3 || EPI == 4 || EPI == 7) && !CHECK && 64 % PR == 0 && IT % 2 == 0) {
+  if constexpr ((EPI == 4 || EPI == 7) && !CHECK && 64 % PR == 0 && IT % 2 == 0) {
     if (args.nt_out) staged_side_out<CF, EPI, S, PR, IT, true>(args, st, sd, mr, nw, lane, cs);
     else staged_side_out<CF, EPI, S, PR, IT, false>(args, st, sd, mr, nw, lane, cs);
     return;
@@ -453,7 +453,10 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
                                int wm, int wn, int wid, int lane, char* smem,
                                unsigned long long* est = nullptr) {
   // EPI 6 / 7: EPI 2 / 4 with GELU' in the fragment order of the W4-256 tiles (frag_aux below)
-  constexpr bool F32 = EPI == 3 || EPI == 4 || EPI == 7;  // staged as fp32 (side input / column sums)
+  // staged as fp32: the GELU' products (row-major side input, or the column sums before rounding).
+  // The residual (EPI 3) is added in the fragment layout before a bf16 staging (same fp32 sum, same
+  // single rounding as adding it to the staged fp32 values; half the LDS passes)
+  constexpr bool F32 = EPI == 4 || EPI == 7;
   constexpr int PL = EPI == 2 ? 2 : 1;           // planes: y (+ GELU' for EPI 2)
   constexpr int S = CF::WTN * (F32 ? 4 : 2) + 16;  // row stride: rows 4 banks apart (b64/b128 writes)
   constexpr int CHF = stage_chf(CF::FM, 16 * S * PL, LDSW);  // fragment rows per pass
@@ -473,7 +476,30 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
     if constexpr (EPI == 1 || EPI == 2 || EPI == 3 || EPI == 6)
       if (args.bias && nb + j * 16 < nlim) bs[j] = *reinterpret_cast<const uint2*>(args.bias + nb + j * 16);
   }
-  const bf16_t* __restrict__ side = EPI == 3 ? args.resid : args.aux;
+  const bool full = nw + CF::WTN <= nlim && mw + CF::WTM <= args.M;  // wave-uniform: no per-piece checks
+  const bf16_t* __restrict__ side = args.aux;
+  // EPI 3: residual pieces of row group i + 1 load while row group i is staged (8 bytes per lane and
+  // fragment: each wave-instruction reads 32 contiguous bytes of 16 rows, the other fragments of the
+  // same lines right behind it)
+  uint2 rsd[EPI == 3 ? 2 : 1][EPI == 3 ? CF::FN : 1];
+  auto resid_load = [&](int i, uint2 (&dst)[EPI == 3 ? CF::FN : 1]) __attribute__((always_inline)) {
+    if constexpr (EPI == 3) {
+      const int m = mw + i * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < CF::FN; ++j) {
+        const int n = nb + j * 16;
+        const bf16_t* p = args.resid + (long)m * args.ldc + n;
+        if (full) {
+          dst[j] = *reinterpret_cast<const uint2*>(p);
+        } else if (m < args.M && n < nlim) {
+          const uint4 t = load8(p, min(4, nlim - n));
+          dst[j] = make_uint2(t.x, t.y);
+        } else {
+          dst[j] = make_uint2(0u, 0u);
+        }
+      }
+    }
+  };
   // fragment-ordered GELU' plane (EPI 6 writes, EPI 7 reads): per 256 x 256 tile 65536 elements in
   // (wave, i, j, lane, 4) order, so each fragment is one fully contiguous 512-byte wave-instruction
   // from the registers (no LDS staging for that plane) and the fc2 data gradient (same W4-256 tile
@@ -482,8 +508,8 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
       ? args.aux + ((long)(m0 / 256) * args.tiles_n + n0 / 256) * 65536 + (long)wid * CF::FM * CF::FN * 256 + lane * 4
       : nullptr;
   const uint32_t dkey = EPI == 3 ? rowdrop_key(eff_seed(args.seed, args.sofs)) : 0u;  // dropout key
-  const bool full = nw + CF::WTN <= nlim && mw + CF::WTM <= args.M;  // wave-uniform: no per-piece checks
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // EPI 4 + dbias: this lane's column sums
+  resid_load(0, rsd[0]);
 #pragma unroll
   for (int c = 0; c < CF::FM / CHF; ++c) {
     // side inputs of this pass first: their latency hides under the LDS staging
@@ -496,7 +522,7 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
         for (int j = 0; j < CF::FN; ++j)
           fx[ii][j] = *reinterpret_cast<const uint2*>(frag_aux + ((c * CHF + ii) * CF::FN + j) * 256);
     }
-    if constexpr (EPI == 3 || EPI == 4) {
+    if constexpr (EPI == 4) {
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
         const int e = it * 64 + lane, r = e / PR, n = nw + (e % PR) * 8;
@@ -511,6 +537,9 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
       const int i = c * CHF + ii;
       const int m = mw + i * 16 + (lane & 15);
       char* row = st + (ii * 16 + (lane & 15)) * S;
+      if constexpr (EPI == 3) {
+        if (i + 1 < CF::FM) resid_load(i + 1, rsd[(i + 1) & 1]);
+      }
 #pragma unroll
       for (int j = 0; j < CF::FN; ++j) {
         const int n = nb + j * 16;
@@ -544,6 +573,9 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
         }
         if constexpr (EPI == 3) {
           if (args.thr) rowdrop4(v, dkey, m, n, args.N, args.thr, args.scale);  // common.h
+          const uint2 rv = rsd[i & 1][j];
+          v[0] += bf2f(rv.x & 0xffffu); v[1] += bf2f(rv.x >> 16);
+          v[2] += bf2f(rv.y & 0xffffu); v[3] += bf2f(rv.y >> 16);
         }
         if constexpr (F32)
           *reinterpret_cast<float4*>(row + col * 4) = make_float4(v[0], v[1], v[2], v[3]);
