@@ -390,7 +390,7 @@ MG_DEVICE void staged_rows(const GemmArgs& args, const char* st, const uint4 (&s
     else staged_copy_out<EPI, S, CHF, PR, IT, false>(args, st, mr, nw, lane);
     return;
   }
-  if constexpr ((EPI == 4 || EPI == 7) && !CHECK && 64 % PR == 0 && IT % 2 == 0) {
+  if constexpr (EPI == 4 && !CHECK && 64 % PR == 0 && IT % 2 == 0) {
     if (args.nt_out) staged_side_out<CF, EPI, S, PR, IT, true>(args, st, sd, mr, nw, lane, cs);
     else staged_side_out<CF, EPI, S, PR, IT, false>(args, st, sd, mr, nw, lane, cs);
     return;
@@ -452,11 +452,12 @@ template <class CF, int EPI, int LDSW>
 MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN], int m0, int n0,
                                int wm, int wn, int wid, int lane, char* smem,
                                unsigned long long* est = nullptr) {
-  // EPI 6 / 7: EPI 2 / 4 with GELU' in the fragment order of the W4-256 tiles (frag_aux below)
-  // staged as fp32: the GELU' products (row-major side input, or the column sums before rounding).
-  // The residual (EPI 3) is added in the fragment layout before a bf16 staging (same fp32 sum, same
-  // single rounding as adding it to the staged fp32 values; half the LDS passes)
-  constexpr bool F32 = EPI == 4 || EPI == 7;
+  // EPI 6 / 7: EPI 2 / 4 with GELU' in the fragment order of the W4-256 tiles (frag_aux below).
+  // Staged as fp32: EPI 4 (its row-major GELU' side input and the bias gradient's column sums act on
+  // the staged values).  The residual (EPI 3) and the fragment-ordered GELU' (EPI 7, whose column sums
+  // then run in the fragment layout too) are applied before a bf16 staging: the same fp32 values and
+  // the same single rounding, half the LDS passes
+  constexpr bool F32 = EPI == 4;
   constexpr int PL = EPI == 2 ? 2 : 1;           // planes: y (+ GELU' for EPI 2)
   constexpr int S = CF::WTN * (F32 ? 4 : 2) + 16;  // row stride: rows 4 banks apart (b64/b128 writes)
   constexpr int CHF = stage_chf(CF::FM, 16 * S * PL, LDSW);  // fragment rows per pass
@@ -481,8 +482,16 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
   // EPI 3: residual pieces of row group i + 1 load while row group i is staged (8 bytes per lane and
   // fragment: each wave-instruction reads 32 contiguous bytes of 16 rows, the other fragments of the
   // same lines right behind it)
-  uint2 rsd[EPI == 3 ? 2 : 1][EPI == 3 ? CF::FN : 1];
-  auto resid_load = [&](int i, uint2 (&dst)[EPI == 3 ? CF::FN : 1]) __attribute__((always_inline)) {
+  constexpr bool ROLL = EPI == 3 || EPI == 7;  // fragment-layout side input, one row group ahead
+  uint2 rsd[ROLL ? 2 : 1][ROLL ? CF::FN : 1];
+  bf16_t* const frag_aux = (EPI == 6 || EPI == 7)
+      ? args.aux + ((long)(m0 / 256) * args.tiles_n + n0 / 256) * 65536 + (long)wid * CF::FM * CF::FN * 256 + lane * 4
+      : nullptr;
+  auto resid_load = [&](int i, uint2 (&dst)[ROLL ? CF::FN : 1]) __attribute__((always_inline)) {
+    if constexpr (EPI == 7) {  // contiguous 512-byte fragments
+#pragma unroll
+      for (int j = 0; j < CF::FN; ++j) dst[j] = *reinterpret_cast<const uint2*>(frag_aux + (i * CF::FN + j) * 256);
+    }
     if constexpr (EPI == 3) {
       const int m = mw + i * 16 + (lane & 15);
 #pragma unroll
@@ -500,28 +509,20 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
       }
     }
   };
-  // fragment-ordered GELU' plane (EPI 6 writes, EPI 7 reads): per 256 x 256 tile 65536 elements in
-  // (wave, i, j, lane, 4) order, so each fragment is one fully contiguous 512-byte wave-instruction
-  // from the registers (no LDS staging for that plane) and the fc2 data gradient (same W4-256 tile
-  // grid and fragment layout) reads exactly the values its lanes need before its own staging
-  bf16_t* const frag_aux = (EPI == 6 || EPI == 7)
-      ? args.aux + ((long)(m0 / 256) * args.tiles_n + n0 / 256) * 65536 + (long)wid * CF::FM * CF::FN * 256 + lane * 4
-      : nullptr;
+  // (frag_aux: the fragment-ordered GELU' plane -- EPI 6 writes, EPI 7 reads -- per 256 x 256 tile
+  // 65536 elements in (wave, i, j, lane, 4) order, so each fragment is one fully contiguous 512-byte
+  // wave-instruction from the registers (no LDS staging for that plane) and the fc2 data gradient
+  // (same W4-256 tile grid and fragment layout) reads exactly the values its lanes need)
   const uint32_t dkey = EPI == 3 ? rowdrop_key(eff_seed(args.seed, args.sofs)) : 0u;  // dropout key
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // EPI 4 + dbias: this lane's column sums
+  float csf[EPI == 7 ? 4 * CF::FN : 1];  // EPI 7: column sums in the fragment layout [j][4]
+#pragma unroll
+  for (int k = 0; k < (EPI == 7 ? 4 * CF::FN : 1); ++k) csf[k] = 0.f;
   resid_load(0, rsd[0]);
 #pragma unroll
   for (int c = 0; c < CF::FM / CHF; ++c) {
     // side inputs of this pass first: their latency hides under the LDS staging
     uint4 sd[F32 ? IT : 1];
-    uint2 fx[EPI == 7 ? CHF : 1][EPI == 7 ? CF::FN : 1];
-    if constexpr (EPI == 7) {  // this pass's GELU' fragments: contiguous 512-byte loads
-#pragma unroll
-      for (int ii = 0; ii < CHF; ++ii)
-#pragma unroll
-        for (int j = 0; j < CF::FN; ++j)
-          fx[ii][j] = *reinterpret_cast<const uint2*>(frag_aux + ((c * CHF + ii) * CF::FN + j) * 256);
-    }
     if constexpr (EPI == 4) {
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
@@ -537,7 +538,7 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
       const int i = c * CHF + ii;
       const int m = mw + i * 16 + (lane & 15);
       char* row = st + (ii * 16 + (lane & 15)) * S;
-      if constexpr (EPI == 3) {
+      if constexpr (ROLL) {
         if (i + 1 < CF::FM) resid_load(i + 1, rsd[(i + 1) & 1]);
       }
 #pragma unroll
@@ -559,9 +560,11 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
                                       reinterpret_cast<v2u*>(frag_aux + (i * CF::FN + j) * 256));
         }
         if constexpr (EPI == 7) {  // x GELU'(z) in the fragment layout (fp32 product, as EPI 4)
-          const uint2 gx = fx[ii][j];
+          const uint2 gx = rsd[i & 1][j];
           v[0] *= bf2f(gx.x & 0xffffu); v[1] *= bf2f(gx.x >> 16);
           v[2] *= bf2f(gx.y & 0xffffu); v[3] *= bf2f(gx.y >> 16);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) csf[j * 4 + e] += v[e];  // fp32, before the rounding
         }
         if constexpr (EPI == 2) {  // y = GELU(z); GELU'(z) into the second plane (packed fp32 math)
           f32x2 y0, y1, g0, g1;
@@ -597,7 +600,41 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
     if (est) est[2] = __builtin_amdgcn_s_memtime();  // staged reads + global stores issued
 #endif
   }
-  if constexpr ((EPI == 4 || EPI == 7) && staged_dbias<CF>()) {
+  if constexpr (EPI == 7) {
+    if (args.dbias) {
+      // the 16 lanes of a column group (lane bits 0-3 = rows) fold by transposing shuffles: lane
+      // (r, g) ends with sums 2 r, 2 r + 1 of its 4 FN values ([j][4]: fragment j, column 4 g + e);
+      // the NWM row-waves meet in LDS, then one atomic per tile column
+      constexpr int NV = 4 * CF::FN;
+      static_assert(NV == 32, "fragment-layout fold: 8 fragments per wave-tile row");
+#pragma unroll
+      for (int M = 8; M >= 1; M >>= 1) {
+        const bool hi = lane & M;
+        const int C = NV * M / 8;
+#pragma unroll
+        for (int i2 = 0; i2 < C / 2; ++i2) {
+          const float send = hi ? csf[i2] : csf[i2 + C / 2];
+          const float keep = hi ? csf[i2 + C / 2] : csf[i2];
+          csf[i2] = keep + __shfl_xor(send, M, 64);
+        }
+      }
+      float* red = reinterpret_cast<float*>(smem);  // [NWM][BN], over the staging regions
+      __syncthreads();  // every wave's staged reads are done
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int idx = 2 * (lane & 15) + t, j = idx / 4, e = idx % 4;
+        red[wm * CF::BN + wn * CF::WTN + 16 * j + 4 * (lane >> 4) + e] = csf[t];
+      }
+      __syncthreads();
+      for (int c = threadIdx.x; c < CF::BN; c += CF::NT) {
+        float t = 0.f;
+#pragma unroll
+        for (int r = 0; r < CF::NWM; ++r) t += red[r * CF::BN + c];
+        if (n0 + c < args.N) atomicAdd(args.dbias + n0 + c, t);
+      }
+    }
+  }
+  if constexpr (EPI == 4 && staged_dbias<CF>()) {
     if (args.dbias) {  // kernel argument: uniform over the workgroup
       // lanes sharing a piece index (lane % PR) fold by shuffles, the NWM row-waves through LDS,
       // then one atomic per tile column with 64 contiguous floats per wave-instruction
