@@ -485,12 +485,16 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
   constexpr bool ROLL = EPI == 3 || EPI == 7;  // fragment-layout side input, one row group ahead
   uint2 rsd[ROLL ? 2 : 1][ROLL ? CF::FN : 1];
   bf16_t* const frag_aux = (EPI == 6 || EPI == 7)
-      ? args.aux + ((long)(m0 / 256) * args.tiles_n + n0 / 256) * 65536 + (long)wid * CF::FM * CF::FN * 256 + lane * 4
+      ? args.aux + ((long)(m0 / 256) * args.tiles_n + n0 / 256) * 65536 + (long)wid * CF::FM * CF::FN * 256 + lane * 8
       : nullptr;
   auto resid_load = [&](int i, uint2 (&dst)[ROLL ? CF::FN : 1]) __attribute__((always_inline)) {
-    if constexpr (EPI == 7) {  // contiguous 512-byte fragments
+    if constexpr (EPI == 7) {  // contiguous 1-KiB fragment pairs
 #pragma unroll
-      for (int j = 0; j < CF::FN; ++j) dst[j] = *reinterpret_cast<const uint2*>(frag_aux + (i * CF::FN + j) * 256);
+      for (int j = 0; j < CF::FN; j += 2) {
+        const uint4 t = *reinterpret_cast<const uint4*>(frag_aux + (i * CF::FN + j) * 256);
+        dst[j] = make_uint2(t.x, t.y);
+        dst[j + 1] = make_uint2(t.z, t.w);
+      }
     }
     if constexpr (EPI == 3) {
       const int m = mw + i * 16 + (lane & 15);
@@ -510,9 +514,10 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
     }
   };
   // (frag_aux: the fragment-ordered GELU' plane -- EPI 6 writes, EPI 7 reads -- per 256 x 256 tile
-  // 65536 elements in (wave, i, j, lane, 4) order, so each fragment is one fully contiguous 512-byte
-  // wave-instruction from the registers (no LDS staging for that plane) and the fc2 data gradient
-  // (same W4-256 tile grid and fragment layout) reads exactly the values its lanes need)
+  // 65536 elements in (wave, i, j / 2, lane, j % 2, 4) order, so each pair of fragments is one fully
+  // contiguous 1-KiB wave-instruction of 16-byte lanes from the registers (no LDS staging for that
+  // plane) and the fc2 data gradient (same W4-256 tile grid and fragment layout) reads exactly the
+  // values its lanes need)
   const uint32_t dkey = EPI == 3 ? rowdrop_key(eff_seed(args.seed, args.sofs)) : 0u;  // dropout key
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // EPI 4 + dbias: this lane's column sums
   float csf[EPI == 7 ? 4 * CF::FN : 1];  // EPI 7: column sums in the fragment layout [j][4]
@@ -541,6 +546,8 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
       if constexpr (ROLL) {
         if (i + 1 < CF::FM) resid_load(i + 1, rsd[(i + 1) & 1]);
       }
+      uint32_t gq[4];  // EPI 6: GELU' of fragments j - 1, j (one 16-byte store per pair)
+      (void)gq;
 #pragma unroll
       for (int j = 0; j < CF::FN; ++j) {
         const int n = nb + j * 16;
@@ -555,9 +562,13 @@ MG_DEVICE void epilogue_staged(const GemmArgs& args, f32x4 (&acc)[CF::FM][CF::FN
           gelu2(f32x2{v[0], v[1]}, y0, g0);
           gelu2(f32x2{v[2], v[3]}, y1, g1);
           v[0] = y0.x; v[1] = y0.y; v[2] = y1.x; v[3] = y1.y;
-          typedef unsigned v2u __attribute__((ext_vector_type(2)));
-          __builtin_nontemporal_store(v2u{pack2(g0.x, g0.y), pack2(g1.x, g1.y)},
-                                      reinterpret_cast<v2u*>(frag_aux + (i * CF::FN + j) * 256));
+          gq[(j & 1) * 2] = pack2(g0.x, g0.y);
+          gq[(j & 1) * 2 + 1] = pack2(g1.x, g1.y);
+          if (j & 1) {
+            typedef unsigned v4u __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(v4u{gq[0], gq[1], gq[2], gq[3]},
+                                        reinterpret_cast<v4u*>(frag_aux + (i * CF::FN + j - 1) * 256));
+          }
         }
         if constexpr (EPI == 7) {  // x GELU'(z) in the fragment layout (fp32 product, as EPI 4)
           const uint2 gx = rsd[i & 1][j];

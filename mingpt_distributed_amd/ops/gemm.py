@@ -30,6 +30,18 @@ def frag_aux_elems(M: int, N: int) -> int:
     return -(-M // 256) * -(-N // 256) * 65536
 
 
+def frag_plane_rowmajor(plane: torch.Tensor, M: int, N: int) -> torch.Tensor:
+    """Row-major [M, N] view of a fragment-ordered plane (a copy; tests and debugging).  Order per
+    256x256 tile: (wave row wm, wave col wn, fragment row i, fragment-column pair jp, lane, jj, 4);
+    lane = 16 g + r holds row 16 i + r, columns 16 (2 jp + jj) + 4 g .. + 3 of its wave's 128^2
+    quadrant (csrc/kernels/gemm.hip, epilogue_staged)."""
+    tm, tn = -(-M // 256), -(-N // 256)
+    v = plane[: tm * tn * 65536].view(tm, tn, 2, 2, 8, 4, 4, 16, 2, 4)
+    # dims: tm tn wm wn i jp g r jj e -> rows (tm wm i r), cols (tn wn jp jj g e)
+    v = v.permute(0, 2, 4, 7, 1, 3, 5, 8, 6, 9).reshape(tm * 256, tn * 256)
+    return v[:M, :N].contiguous()
+
+
 def frag_aux_ok(M: int, N: int, K: int) -> bool:
     """The fragment-ordered GELU' plane (epilogues 6 / 7) needs producer and consumer on the same
     256x256 tile grid: true when the dispatcher would pick W4-256 for both the forward [M, N, K]

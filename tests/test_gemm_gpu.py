@@ -226,6 +226,7 @@ def test_fragment_ordered_gelu_plane(M, tile_config):
     y1 = G.gemm_nt(x, w, bias=b, epi="gelu", pre_out=fr, frag=True)
     if tile_config in (0, 5):  # the same W4-256 kernel on both sides: bitwise
         assert torch.equal(y1, y0)
+        assert torch.equal(G.frag_plane_rowmajor(fr, M, Nout), pre)  # the documented order
     else:
         torch.testing.assert_close(y1, y0, atol=2e-2, rtol=2e-2)
     db0 = torch.zeros(Nout, device=DEV)
