@@ -30,7 +30,7 @@ def timeit(fn, iters=20, warm=3):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--tokens", type=int, default=32768)
+    ap.add_argument("--tokens", type=int, default=131072)
     ap.add_argument("--D", type=int, default=768)
     a = ap.parse_args()
     M, D = a.tokens, a.D
@@ -50,6 +50,14 @@ def main():
             "resid_p0.1": timeit(lambda: G.gemm_nt(x, w, bias=b, epi="resid", resid=res, p=0.1, seed=5)),
             "gelu_bwd": timeit(lambda: G.gemm_nt(x, w, epi="gelu_bwd", aux=g)),
         }
+        if G.frag_aux_ok(M, N, K):  # the fragment-ordered GELU' plane (epilogues 6 / 7)
+            fr = torch.empty(G.frag_aux_elems(M, N), device="cuda", dtype=torch.bfloat16)
+            G.gemm_nt(x, w, bias=b, epi="gelu", pre_out=fr, frag=True)
+            t["gelu_frag"] = timeit(lambda: G.gemm_nt(x, w, bias=b, epi="gelu", pre_out=fr, frag=True))
+            # the data gradient through that plane: dz [M, K] = (dy [M, N] x W [N, K]) * GELU'
+            dy, wn = r(M, K), r(K, N)
+            t["dgrad_none(NN)"] = timeit(lambda: G.gemm_nn(dy, wn))
+            t["dgrad_gelu_bwd_frag(NN)"] = timeit(lambda: G.gemm_nn(dy, wn, epi="gelu_bwd", aux=fr, aux_frag=True))
         fl = 2.0 * M * N * K
         out[f"{name}(M={M},N={N},K={K})"] = {k: [round(v * 1e3, 1), round(fl / v / 1e9)] for k, v in t.items()}
     print(json.dumps({"epilogue_us_tflops": out}))
