@@ -129,7 +129,13 @@ class PhaseWatchdog:
                             else "; every gradient collective of the last step completed")
             except Exception as e:  # noqa: BLE001 -- diagnostics only
                 msg += f"; (collective state unavailable: {e})"
-            print(msg + " -- exiting", file=sys.stderr, flush=True)
+            # a grace period before exiting: the first rank to exit makes torchrun SIGTERM the
+            # others, whose own watchdogs (same limit, phases entered within a poll or two) would
+            # otherwise be killed before printing their diagnosis -- usually the informative one
+            # (the healthy rank blocked in the collective names the bucket)
+            grace = min(10.0, max(3.0, 0.25 * lim))
+            print(msg + f" -- exiting in {grace:.0f} s", file=sys.stderr, flush=True)
+            time.sleep(grace)
             os._exit(EXIT_HANG)
 
 

@@ -68,8 +68,9 @@ class ZeroGradEngine(DataParallelEngine):
             self.own.append((lo, lo + sh))
         self.shard_numel = sum(hi - lo for lo, hi in self.own)
         self.gather_work: List[Optional[object]] = [None] * len(self.buckets)
-        # gloo (CPU tests, or device tensors staged through the host) has no in-place
-        # reduce-scatter: it all-reduces the whole bucket (2x the traffic, same result)
+        # gloo (CPU tests, and two ranks sharing one GPU in tests/test_dp_gpu.py) runs the same
+        # in-place reduce_scatter_tensor / all_gather_into_tensor calls as RCCL (torch >= 2.6 has
+        # both on gloo, host and device tensors); only consolidate()'s gather needs host tensors
         self._gloo = multi and dist.get_backend(process_group) == "gloo"
         self._hook_handle = None
         # Per-bucket waits are only sound when every weight read of a grad-enabled GPU forward
@@ -87,8 +88,6 @@ class ZeroGradEngine(DataParallelEngine):
     # ------------------------------------------------------------------ gradients
     def _issue(self, b: _Bucket, wire: Optional[torch.Tensor] = None):
         wire = self._wire(b) if wire is None else wire
-        if self._gloo:
-            return dist.all_reduce(wire, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
         bi = self.buckets.index(b)
         lo, hi = self.own[bi]
         out = wire[lo - b.start:hi - b.start]
@@ -102,10 +101,9 @@ class ZeroGradEngine(DataParallelEngine):
         super().finish()
 
     def bus_bytes(self, b: _Bucket) -> float:
-        """Reduce-scatter: (N-1)/N x bucket bytes per rank (gloo runs an all-reduce: 2x that)."""
+        """Reduce-scatter: (N-1)/N x bucket bytes per rank."""
         esz = 2 if self.reduce_dtype == torch.bfloat16 else 4
-        k = 2.0 if self._gloo else 1.0
-        return k * (self.world - 1) / self.world * (b.end - b.start) * esz
+        return (self.world - 1) / self.world * (b.end - b.start) * esz
 
     def relayout_order(self):
         self.observed = None  # moments are sharded by layout position: keep the layout
@@ -120,11 +118,7 @@ class ZeroGradEngine(DataParallelEngine):
         for bi, b in enumerate(self.buckets):
             lo, hi = self.own[bi]
             full = flat[b.start:b.end]
-            if self._gloo:
-                shard = flat[lo:hi].clone()
-                self.gather_work[bi] = dist.all_gather(list(full.chunk(self.world)), shard,
-                                                       group=self.pg, async_op=True)
-            elif self.native is not None:
+            if self.native is not None:
                 self.gather_work[bi] = self.native.all_gather(flat[lo:hi], full)
             else:
                 self.gather_work[bi] = dist.all_gather_into_tensor(full, flat[lo:hi], group=self.pg,
@@ -156,9 +150,7 @@ class ZeroGradEngine(DataParallelEngine):
         for bi, b in enumerate(self.buckets):
             lo, hi = self.own[bi]
             full = buf[b.start:b.end]
-            if self._gloo:
-                dist.all_gather(list(full.chunk(self.world)), buf[lo:hi].clone(), group=self.pg)
-            elif self.native is not None:
+            if self.native is not None:
                 self.native.all_gather(buf[lo:hi], full).wait()
             else:
                 dist.all_gather_into_tensor(full, buf[lo:hi], group=self.pg)
