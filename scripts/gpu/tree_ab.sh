@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 5, call 4: GPU suite, bench A/B against a base tree snapshot, kernel table.
-#   scripts/gpu/r5_call4.sh BASE_TREE_DIR
+# GPU suite, bench A/B of the tree against a base tree snapshot (scripts/build_ab_tree.sh), kernel table.
+#   TAG=x scripts/gpu/tree_ab.sh BASE_TREE_DIR
 set -o pipefail
 cd "$(dirname "$0")/../.."
-BASE=$1; OUT=gpurun_out/${TAG:-r5c4}; mkdir -p "$OUT"; export TMPDIR=/tmp
+BASE=$1; OUT=gpurun_out/${TAG:-treeab}; mkdir -p "$OUT"; export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/ -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/tests.log" 2>&1
 s=$?; tail -3 "$OUT/tests.log"
 if [ $s -ne 0 ] && [ $s -ne 1 ]; then exit $s; fi
