@@ -135,7 +135,8 @@ class PhaseWatchdog:
             # (the healthy rank blocked in the collective names the bucket)
             grace = min(10.0, max(3.0, 0.25 * lim))
             print(msg + f" -- exiting in {grace:.0f} s", file=sys.stderr, flush=True)
-            time.sleep(grace)
+            if self._stop.wait(grace):  # the run finished meanwhile: stop() joins this thread
+                return
             os._exit(EXIT_HANG)
 
 
