@@ -10,7 +10,7 @@
 from __future__ import annotations
 
 import math
-from typing import Iterator, Optional
+from typing import Iterator
 
 import torch
 from torch.utils.data import Sampler

@@ -23,7 +23,7 @@ from .data import CharDataset, DataConfig, SyntheticTokens
 from .models import GPT, GPTConfig, OptimizerConfig
 from .optim import create_optimizer
 from .parallel import dist as D
-from .trainer import GPTTrainer, GPTTrainerConfig
+from .trainer import GPTTrainer
 from .utils.config import load_run_config
 
 
