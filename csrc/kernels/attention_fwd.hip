@@ -246,13 +246,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const AttnArgs a) {
   const long ld = 3L * a.D;
   const bf16_t* Qg = a.qkv + (long)b * a.T * ld + hh * a.hd;
   const bf16_t* Kg = Qg + a.D;
-  const bf16_t* Vg = Qg + 2 * a.D;
   // the pair's query blocks, heavier first; the middle block of an odd count runs alone
   const int qbA = nqb - 1 - pr, qbB = pr;
   const bool two = MG_FWD_PAIR && qbB < qbA;
   const int ntA = (min(a.T, qbA * 128 + 128) + 63) / 64;
   const int ntB = two ? (min(a.T, qbB * 128 + 128) + 63) / 64 : 0;
-  const int ng = (a.T + 31) / 32, nt = (a.T + 63) / 64;
+  const int nt = (a.T + 63) / 64;
 
   // tile staging: chunk c of this thread -> (half, row, 16-byte column chunk), offsets once.  The
   // loads are buffer loads through a per-tile descriptor (base = the tile's first key row, extent

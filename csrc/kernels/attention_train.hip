@@ -626,17 +626,6 @@ constexpr int bwd_smem() {
 
 int nks_for_bwd(int hd) { return nks_for(hd); }
 
-int num_cus() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    if (n <= 0) n = 256;
-  }
-  return n;
-}
-
 int bwd_keys_per_block(int hd) { return nks_for_bwd(hd) > 4 ? 128 : 256; }
 
 // Key-block mode (one workgroup per (key block, b, h), heaviest key blocks first, then a finalize

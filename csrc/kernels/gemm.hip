@@ -193,12 +193,7 @@ struct Stager {
 MG_DEVICE uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
-MG_DEVICE s16x4 ds_read_tr16(const char* p) {
-  s16x4 r;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_addr(p)));
-  return r;
-}
-// the same with a constant byte offset in the instruction's offset field (no address VALU)
+// ds_read_b64_tr_b16 with a constant byte offset in the instruction's offset field (no address VALU)
 template <int OFF>
 MG_DEVICE s16x4 ds_read_tr16_off(uint32_t addr) {
   static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
@@ -213,25 +208,11 @@ MG_DEVICE void lds_ready(bf16x8 (&f)[N], bool wait = true) {
   for (int i = 0; i < N; ++i) asm volatile("" : "+v"(f[i]));
 }
 
-// ---- fragment read for 16-wide subtile sb, k-step ks (32 k)
-template <bool KC>
-MG_DEVICE bf16x8 frag(const char* lds, int sb, int ks, int lane) {
-  if constexpr (KC) {
-    const int row = sb * 16 + (lane & 15);
-    const int ch = ks * 4 + (lane >> 4);
-    return *reinterpret_cast<const bf16x8*>(lds + row * 128 + ((ch ^ (row & 7)) << 4));
-  } else {
-    const char* img = lds + (sb >> 3) * 16384;
-    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-    const int chk = (sb & 7) * 2 + (p >> 1);
-    const int r0 = ks * 32 + 8 * g + q, r1 = r0 + 4;
-    const char* a0 = img + r0 * 256 + ((chk ^ swz_mn(r0)) << 4) + (p & 1) * 8;
-    const char* a1 = a0 + (r1 - r0) * 256;  // swz_mn(r0 + 4) == swz_mn(r0)
-    const s16x4 x = ds_read_tr16(a0);
-    const s16x4 y = ds_read_tr16(a1);
-    const s16x8 v = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
-    return __builtin_bit_cast(bf16x8, v);
-  }
+// ---- fragment read of a k-contiguous image for 16-wide subtile sb, k-step ks (32 k)
+MG_DEVICE bf16x8 frag_kc(const char* lds, int sb, int ks, int lane) {
+  const int row = sb * 16 + (lane & 15);
+  const int ch = ks * 4 + (lane >> 4);
+  return *reinterpret_cast<const bf16x8*>(lds + row * 128 + ((ch ^ (row & 7)) << 4));
 }
 
 // frag with the k-step a template constant (W4): for m/n-contiguous images the k-step and the
@@ -242,7 +223,7 @@ MG_DEVICE bf16x8 frag(const char* lds, int sb, int ks, int lane) {
 template <bool KC, int KS, int HS = 16384, int OFF = 0>
 MG_DEVICE bf16x8 frag_k(const char* lds, int sb, int lane) {
   if constexpr (KC) {
-    return frag<true>(lds + OFF, sb, KS, lane);
+    return frag_kc(lds + OFF, sb, KS, lane);
   } else {
     const char* img = lds + (sb >> 3) * HS;
     const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;

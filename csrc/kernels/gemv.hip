@@ -38,14 +38,6 @@ MG_DEVICE unsigned long long amax_key(float v, int n) {
   return ((unsigned long long)k << 32) | (uint32_t)(0xffffffffu - (uint32_t)n);
 }
 MG_DEVICE unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
-MG_DEVICE unsigned long long wave_umax64(unsigned long long v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned lo = __shfl_xor((unsigned)v, o, 64), hi = __shfl_xor((unsigned)(v >> 32), o, 64);
-    v = umax64(v, ((unsigned long long)hi << 32) | lo);
-  }
-  return v;
-}
 
 // Fused greedy argmax, first half: every workgroup publishes its best (value, index) key per row
 // to part[b][workgroup] with plain stores, and workgroup 0 advances the device position.  The
