@@ -27,10 +27,12 @@
 //  * operands swapped in the MFMA (C^T = B'^T A'^T): each lane holds 4 consecutive n of one row m,
 //    so epilogue stores are 8 B (bf16) / 16 B (fp32).
 //  * XCD-aware bijective block remap + GROUP_M ordering (blocks sharing A rows share an XCD's L2).
-//  * epilogues: none | +bias | +bias,GELU (GELU'(z) also stored) |
-//    resid + dropout(acc + bias) (counter-hash row-block mask, common.h) |
-//    acc * aux (GELU' from the forward, + the fc bias gradient's column sums) | fp32 accumulate
-//    (the main-grad buffer), split-K via LDS-staged atomics.
+//  * epilogues: none | +bias | +bias,GELU (GELU'(z) also stored: row-major, or in the W4 tiles'
+//    fragment order straight from the registers, EPI 6) | resid + dropout(acc + bias) (counter-hash
+//    row-block mask, common.h; the residual added in the fragment layout) | acc * GELU' (+ the fc
+//    bias gradient's column sums; row-major EPI 4 or fragment-ordered EPI 7) | fp32 accumulate
+//    (the main-grad buffer), split-K via atomics.  bf16 outputs leave through a per-wave LDS
+//    staging as 16-byte pieces of whole rows (epilogue_staged).
 #include "common.h"
 #include "kernels.h"
 #include <type_traits>
@@ -1220,7 +1222,7 @@ int pick_config(int M, int N, int K, int layout) {
     return r192 * 108 < r256 * 100 ? 6 : 5;
   }
   // dgrad (NN, the weight read in place through the transposing LDS reads): W4 at every block
-  // shape (bench/dgrad_nn_vs_nt.py, M = 65536: proj 84 / PP 97 us, fc 251 / 290, qkv 182 / 210,
+  // shape (bench/dgrad_nn_vs_nt.py, M = 65536, W4 / the deleted ping-pong: proj 84 / 97 us, fc 251 / 290, qkv 182 / 210,
   // fc2 + GELU' 344 / 362), and faster than NT against a transposed weight copy
   if (layout == 1) return t256 >= 256 ? 5 : 1;
   // tiny outputs (gpt-mini) on T128; from 512 x 512 up the split-K cost model decides: the 768 x 768
