@@ -24,6 +24,7 @@ from __future__ import annotations
 import contextlib
 import io
 import os
+import shutil
 import time
 from collections import defaultdict
 from dataclasses import asdict, dataclass
@@ -382,18 +383,57 @@ class ModelSnapshot:
     rng_state: Optional[torch.Tensor] = None
 
 
+def _is_local(fs) -> bool:
+    proto = fs.protocol if isinstance(fs.protocol, str) else fs.protocol[0]
+    return proto in ("file", "local")
+
+
 def _atomic_save(obj, path: str):
-    """Write to ``path.tmp`` then rename: a crash mid-write never leaves a torn snapshot."""
+    """Crash-safe snapshot write (replaces the reference's plain ``torch.save``,
+    ``/root/reference/mingpt/trainer.py:149-167``).
+
+    1. the bytes go to ``path.tmp`` (fsynced on a local / Lustre path);
+    2. the current snapshot, if any, is kept as ``path.prev`` (a hard link where the filesystem
+       has them, else a copy) -- ``path`` itself is never removed;
+    3. ``path.tmp`` replaces ``path`` by one atomic rename (``os.replace``); object stores, whose
+       ``mv`` has no rm window to begin with, go through fsspec.
+
+    A crash at any point leaves ``path`` (old or new, never torn or missing) or, at worst, the
+    previous snapshot in ``path.prev``, which ``GPTTrainer._load_snapshot`` falls back to."""
     import fsspec
 
     fs, p = fsspec.core.url_to_fs(path)
-    tmp = p + ".tmp"
+    tmp, prev = p + ".tmp", p + ".prev"
     buf = io.BytesIO()
     torch.save(obj, buf)
+    if _is_local(fs):
+        d = os.path.dirname(os.path.abspath(p))
+        os.makedirs(d, exist_ok=True)
+        with open(tmp, "wb") as f:
+            f.write(buf.getvalue())
+            f.flush()
+            os.fsync(f.fileno())
+        if os.path.exists(p):
+            if os.path.lexists(prev):
+                os.remove(prev)
+            try:
+                os.link(p, prev)
+            except OSError:  # no hard links here (some network filesystems): copy
+                shutil.copyfile(p, prev)
+        os.replace(tmp, p)
+        try:  # persist the rename itself
+            fd = os.open(d, os.O_RDONLY)
+            try:
+                os.fsync(fd)
+            finally:
+                os.close(fd)
+        except OSError:
+            pass
+        return
     with fs.open(tmp, "wb") as f:
         f.write(buf.getvalue())
     if fs.exists(p):
-        fs.rm(p)
+        fs.copy(p, prev)
     fs.mv(tmp, p)
 
 
@@ -479,10 +519,24 @@ class GPTTrainer:
     def _load_snapshot(self):
         import fsspec
 
-        try:
-            with fsspec.open(self.config.snapshot_path, "rb") as f:
-                data = torch.load(f, map_location="cpu", weights_only=True)
-        except FileNotFoundError:
+        # the snapshot, else the one _atomic_save kept before it (a crash inside a save, or a
+        # snapshot that no longer loads); nothing found at either: train from scratch
+        data, errors = None, []
+        for cand in (self.config.snapshot_path, self.config.snapshot_path + ".prev"):
+            try:
+                with fsspec.open(cand, "rb") as f:
+                    data = torch.load(f, map_location="cpu", weights_only=True)
+            except FileNotFoundError:
+                continue
+            except Exception as e:  # torn / unreadable file: try the previous one
+                errors.append(f"{cand}: {type(e).__name__}: {e}")
+                continue
+            if cand != self.config.snapshot_path and self.global_rank == 0:
+                print(f"Snapshot {self.config.snapshot_path} missing or unreadable; resuming from {cand}")
+            break
+        if data is None:
+            if errors:  # snapshots exist but none loads: never silently start over
+                raise RuntimeError("no loadable snapshot: " + "; ".join(errors))
             if self.global_rank == 0:
                 print("Model snapshot not found. Training from scratch.")
             return

@@ -49,6 +49,55 @@ def test_gpt_trainer_trains_and_snapshots(tmp_path):
     assert [h["epoch"] for h in tr2.history] == [2]
 
 
+class _KilledInSave(BaseException):
+    pass
+
+
+def test_snapshot_save_killed_before_rename_resumes_previous(tmp_path, monkeypatch):
+    """A process killed inside a save, after the temp write and before the rename, leaves the
+    previous snapshot in place: the next run resumes from it instead of training from scratch."""
+    cfg, model, opt, train, test = _setup(tmp_path, max_epochs=2)
+    real_replace, calls = os.replace, []
+
+    def dying_replace(src, dst):
+        calls.append(dst)
+        if len(calls) == 2:  # the epoch-1 save
+            raise _KilledInSave()
+        return real_replace(src, dst)
+
+    monkeypatch.setattr(os, "replace", dying_replace)
+    with pytest.raises(_KilledInSave):
+        GPTTrainer(cfg, model, opt, train, None).train()
+    monkeypatch.setattr(os, "replace", real_replace)
+    assert os.path.exists(cfg.snapshot_path) and os.path.exists(cfg.snapshot_path + ".tmp")
+    assert torch.load(cfg.snapshot_path, weights_only=True)["final_epoch"] == 0
+    cfg2, model2, opt2, train2, _ = _setup(tmp_path, max_epochs=2)
+    tr2 = GPTTrainer(cfg2, model2, opt2, train2, None)
+    assert tr2.last_epoch == 0 and tr2.step == 20
+    tr2.train()
+    assert [h["epoch"] for h in tr2.history] == [1]
+    assert not os.path.exists(cfg.snapshot_path + ".tmp")
+
+
+def test_snapshot_unreadable_falls_back_to_prev(tmp_path):
+    cfg, model, opt, train, test = _setup(tmp_path, max_epochs=2)
+    GPTTrainer(cfg, model, opt, train, None).train()
+    p = cfg.snapshot_path
+    assert torch.load(p + ".prev", weights_only=True)["final_epoch"] == 0
+    assert torch.load(p, weights_only=True)["final_epoch"] == 1
+    blob = open(p, "rb").read()
+    with open(p, "wb") as f:  # torn write of the latest snapshot
+        f.write(blob[: len(blob) // 3])
+    cfg2, model2, opt2, train2, _ = _setup(tmp_path, max_epochs=2)
+    tr2 = GPTTrainer(cfg2, model2, opt2, train2, None)
+    assert tr2.last_epoch == 0 and tr2.step == 20
+    with open(p + ".prev", "wb") as f:  # nothing loadable: refuse to start over silently
+        f.write(b"garbage")
+    cfg3, model3, opt3, train3, _ = _setup(tmp_path, max_epochs=2)
+    with pytest.raises(RuntimeError, match="no loadable snapshot"):
+        GPTTrainer(cfg3, model3, opt3, train3, None)
+
+
 def test_snapshot_memory_fs(tmp_path):
     cfg, model, opt, train, test = _setup(tmp_path, snapshot="memory://ckpt/snap.pt", max_epochs=1)
     GPTTrainer(cfg, model, opt, train, None).train()
