@@ -63,6 +63,7 @@ std::vector<at::Tensor> layernorm_bwd(const at::Tensor& dy, const at::Tensor& x,
   const int64_t D = x.size(-1), M = x.numel() / D;
   TORCH_CHECK(dy.numel() == x.numel() && dw.numel() == D && db.numel() == D && mean.numel() == M,
               "layernorm_bwd: shape mismatch");
+  TORCH_CHECK(D % 8 == 0 && D <= 4096, "layernorm_bwd: D must be a multiple of 8, at most 4096");
   DevGuard g(x.device());
   auto dx = at::empty_like(x);
   if (dres.has_value() && dres->defined()) {
@@ -76,7 +77,7 @@ std::vector<at::Tensor> layernorm_bwd(const at::Tensor& dy, const at::Tensor& x,
     TORCH_CHECK(dz_bias->numel() == D && D % 8 == 0, "layernorm_bwd: dz_bias must be fp32 [D]");
     dz = at::empty_like(x);
   }
-  auto ws = at::empty({(int64_t)mg::layernorm_bwd_workspace((int)M, (int)D)}, mean.options());
+  auto ws = at::empty({(int64_t)mg::layernorm_bwd_workspace((int)M, (int)D, drop)}, mean.options());
   mg::layernorm_bwd(bp(dy), bp(x), bp(w), fp(mean), fp(rstd), bp_opt(dres), bp(dx), fp(dw), fp(db), fp(ws),
                     (int)M, (int)D, cur_stream(), drop ? bp(dz) : nullptr, drop ? fp(*dz_bias) : nullptr,
                     (float)drop_p, (uint64_t)drop_seed);

@@ -18,7 +18,7 @@ void layernorm_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const flo
                    const float* rstd, const bf16_t* dres, bf16_t* dx, float* dw, float* db,
                    float* workspace, int M, int D, hipStream_t stream, bf16_t* dz = nullptr,
                    float* dzb = nullptr, float p = 0.f, uint64_t seed = 0);
-size_t layernorm_bwd_workspace(int M, int D);
+size_t layernorm_bwd_workspace(int M, int D, bool drop);
 
 // embedding.hip
 void embedding_fwd(const int64_t* idx, const bf16_t* wte, const bf16_t* wpe, bf16_t* out, int M,

@@ -218,26 +218,27 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       }
     }
   }
-  // fold the 4 waves' column partials through LDS and store the block's partial row
-  // [dgamma | dbeta] with plain stores; ln_colsum_kernel adds the blocks up (a single-stage
-  // atomic fold put every block's atomics on the same 2D addresses)
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [4][NP*D]
+  // fold the 4 waves' column partials through LDS, one plane at a time, and store the block's
+  // partial row [dgamma | dbeta (| dbias)] with plain stores; ln_colsum_kernel adds the blocks up
+  // (a single-stage atomic fold put every block's atomics on the same 2D addresses).  One plane
+  // of LDS (16 D bytes, 64 KiB at D = 4096) for any NP: all planes at once needed 48 D bytes with
+  // the dropout plane, past the 160 KiB LDS for D > 3413.
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [4][D]
+  float* prow = part + (long)blockIdx.x * NP * D;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = (i * 64 + lane) * 8;
-    if (c < D) {
+  for (int k = 0; k < NP; ++k) {
+    if (k) __syncthreads();  // the previous plane's readers are done
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        red[wid * NP * D + c + j] = gacc[i][j];
-        red[wid * NP * D + D + c + j] = bacc[i][j];
-        if constexpr (DROP) red[wid * NP * D + 2 * D + c + j] = zacc[i][j];
+    for (int i = 0; i < NV; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      if (c < D) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) red[wid * D + c + j] = k == 0 ? gacc[i][j] : k == 1 ? bacc[i][j] : zacc[DROP ? i : 0][j];
       }
     }
+    __syncthreads();
+    for (int c = threadIdx.x; c < D; c += 256) prow[k * D + c] = red[c] + red[D + c] + red[2 * D + c] + red[3 * D + c];
   }
-  __syncthreads();
-  float* prow = part + (long)blockIdx.x * NP * D;
-  for (int c = threadIdx.x; c < NP * D; c += 256)
-    prow[c] = red[c] + red[NP * D + c] + red[2 * NP * D + c] + red[3 * NP * D + c];
 }
 
 // dw += sum over blocks of part[:, :D], db += ... part[:, D:].  Block = 64 columns x 4 waves over a
@@ -272,24 +273,30 @@ namespace mg {
 // >= 32 rows per block (4 waves x 2 rows x >= 4 iterations) up to 1024 blocks
 // One resident wave of blocks: the kernel grid-strides over rows, and a grid of more blocks than
 // fit the CUs at once (1024 at D = 768, where 150 VGPRs leave room for 3 blocks per CU = 768)
-// ran a second, one-third-full round.  Occupancy from the runtime for the instantiation D selects.
-template <int NV>
+// ran a second, one-third-full round.  Occupancy from the runtime for the instantiation (D, and
+// with or without the fused dropout plane) the launch selects.
+template <int NV, bool DROP>
 static int ln_bwd_resident() {
   static int n = 0;
   if (!n) {
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)ln_bwd_kernel<NV, true>, 256,
-                                                       sizeof(float) * 12 * NV * 512);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)ln_bwd_kernel<NV, DROP>, 256,
+                                                       sizeof(float) * 4 * NV * 512);
     n = std::max(1, cus * std::max(1, per_cu));
   }
   return n;
 }
 
-int ln_bwd_grid(int M, int D) {
-  const int cap = D <= 512 ? ln_bwd_resident<1>() : D <= 1024 ? ln_bwd_resident<2>()
-                  : D <= 2048 ? ln_bwd_resident<4>() : ln_bwd_resident<8>();
+template <bool DROP>
+static int ln_bwd_cap(int D) {
+  return D <= 512 ? ln_bwd_resident<1, DROP>() : D <= 1024 ? ln_bwd_resident<2, DROP>()
+         : D <= 2048 ? ln_bwd_resident<4, DROP>() : ln_bwd_resident<8, DROP>();
+}
+
+int ln_bwd_grid(int M, int D, bool drop) {
+  const int cap = drop ? ln_bwd_cap<true>(D) : ln_bwd_cap<false>(D);
   return std::max(1, std::min(M / 32, cap));
 }
 
@@ -312,10 +319,10 @@ void layernorm_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const flo
                    const float* rstd, const bf16_t* dres, bf16_t* dx, float* dw, float* db,
                    float* workspace, int M, int D, hipStream_t stream, bf16_t* dz, float* dzb, float p,
                    uint64_t seed) {
-  const int grid = ln_bwd_grid(M, D);
   const bool drop = dz != nullptr;
+  const int grid = ln_bwd_grid(M, D, drop);
   const int NP = drop ? 3 : 2;
-  const size_t smem = sizeof(float) * 4 * NP * D;
+  const size_t smem = sizeof(float) * 4 * D;  // one partial plane at a time
   const uint32_t thr = drop ? dropout_threshold16(p) : 0u;
   const LnDrop dr{dz, seed, graph_seed_ofs(), thr, dropout_scale16(thr)};
 #define MG_LN_BWD(NV)                                                                                   \
@@ -329,7 +336,9 @@ void layernorm_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* w, const flo
   ln_colsum_kernel<<<dim3(cdiv(NP * D, 64), cdiv(grid, 32)), 256, 0, stream>>>(workspace, grid, D, NP, dw, db, dzb);
 }
 
-// floats of partial [dgamma | dbeta | dbias] rows layernorm_bwd needs
-size_t layernorm_bwd_workspace(int M, int D) { return (size_t)ln_bwd_grid(M, D) * 3 * D; }
+// floats of partial [dgamma | dbeta (| dbias)] rows layernorm_bwd needs
+size_t layernorm_bwd_workspace(int M, int D, bool drop) {
+  return (size_t)ln_bwd_grid(M, D, drop) * (drop ? 3 : 2) * D;
+}
 
 }  // namespace mg
