@@ -97,6 +97,11 @@ class Block(nn.Module):
 class GPT(nn.Module):
     """GPT Language Model."""
 
+    # GPU training path: run each block's MLP residual-dropout backward inside its consumer's
+    # LayerNorm backward (ops/fused.py DropLink).  False = every block runs its own
+    # dropout_bias_grad pass (same masks, same gradients; the tests compare the two).
+    dropout_handoff = True
+
     @staticmethod
     def get_default_config() -> CfgNode:
         """Upstream-minGPT style config node (``model_type='gpt'`` with dims None)."""
@@ -193,7 +198,7 @@ class GPT(nn.Module):
         # residual-dropout hand-offs: block l's MLP dropout backward runs inside the LayerNorm
         # backward of its consumer (block l+1's ln_1, or ln_f) -- ops/fused.py DropLink
         link = None
-        fuse = self.training and torch.is_grad_enabled() and c.resid_drop > 0
+        fuse = self.dropout_handoff and self.training and torch.is_grad_enabled() and c.resid_drop > 0
         for block in tr.h:
             out = DropLink(0.0, 0, _bf16(block.mlp.c_proj.bias)) if fuse else None
             x = block(x, _links=(link, out))
