@@ -1,0 +1,31 @@
+"""Per-tile phase times of attn_bwd64_kernel from a -DMG_BWD64_STAMPS build (s_memtime per wave at
+8 points of each tile of the first 64 workgroups = key block 0 at the GPT-2 B = 128 shape):
+    MINGPT_EXT_SO=build/ab/stamps/_C.so python bench/dev/bwd64_stamps.py"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch
+
+from mingpt_distributed_amd.ops._ext import ext
+
+C = ext()
+B, T, H, hd = int(os.environ.get("ATTN_B", "128")), 1024, 12, 64
+D = H * hd
+qkv = torch.randn(B * T, 3 * D, device="cuda").to(torch.bfloat16)
+dout = torch.randn(B * T, D, device="cuda").to(torch.bfloat16)
+out, lse, mask = C.attention_fwd(qkv, B, T, H, 0.1, 1)
+for _ in range(4):
+    C.attention_bwd(qkv, out, dout, lse, mask, B, T, H, 0.1, 1)
+torch.cuda.synchronize()
+st = C.attention_bwd64_stamps().view(64, 4, 8, 8).double()
+names = ["issue", "tile body", "barrier 1", "commit", "dQ MFMA", "dQ store", "barrier 2"]
+print("phase cycles (median over workgroups and waves), tiles 0-1 diagonal, 2-7 steady")
+print(f"{'tile':>4s} " + " ".join(f"{n:>10s}" for n in names) + f" {'total':>8s}")
+for t in range(8):
+    d = st[:, :, t, 1:] - st[:, :, t, :-1]
+    med = d.reshape(-1, 7).median(0).values
+    tot = (st[:, :, t, 7] - st[:, :, t, 0]).median().item()
+    print(f"{t:4d} " + " ".join(f"{v:10.0f}" for v in med.tolist()) + f" {tot:8.0f}")
+nxt = (st[:, :, 1:, 0] - st[:, :, :-1, 7]).median().item()
+print(f"between tiles (loop overhead): {nxt:.0f}")

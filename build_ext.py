@@ -31,6 +31,10 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result",
                 "-I" + os.path.join(ROOT, "csrc", "include"), "-ffp-contract=fast"]
+# per-source extras.  attention_train.hip: no SLP vectoriser -- it packs the softmax-gradient
+# multiplies into v_pk_mul/fma_f32 pairs with s_nop between them, an anti-lever beside MFMAs
+# (MI355X_MICROARCH 'price of one filler'), and the hd = 64 backward's register budget is tight
+FILE_FLAGS = {"attention_train.hip": ["-fno-slp-vectorize"]}
 
 
 
@@ -71,7 +75,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True, debug: bool 
     # the objects' compile flags (MG_EXTRA_FLAGS variant switches included): a change rebuilds
     # every object, so a variant build never leaves objects a later plain build would link
     stamp = os.path.join(bdir, "flags.stamp")
-    key = " ".join(flags)
+    key = " ".join(flags) + " " + repr(sorted(FILE_FLAGS.items()))
     old = open(stamp).read() if os.path.exists(stamp) else None
     if old != key:
         force = True
@@ -87,7 +91,8 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True, debug: bool 
         obj = os.path.join(bdir, os.path.basename(src) + ".o")
         objs.append(obj)
         if force or _newer(obj, [src] + headers):
-            jobs_list.append([HIPCC, *flags, "-x", "hip", "-c", "-o", obj, src])
+            jobs_list.append([HIPCC, *flags, *FILE_FLAGS.get(os.path.basename(src), []), "-x", "hip", "-c",
+                              "-o", obj, src])
     bsrc = os.path.join(ROOT, "csrc", "bindings.cpp")
     bobj = os.path.join(bdir, "bindings.o")
     objs.append(bobj)

@@ -701,6 +701,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_get_variant", &mg::gemm_get_variant);
   m.def("gemm_pick", &mg::gemm_pick, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("layout"));
   m.def("attention_set_bwd_mode", &mg::attention_set_bwd_mode);
+  m.def("attention_set_bwd64", &mg::attention_set_bwd64);
+#ifdef MG_BWD64_STAMPS
+  m.def("attention_bwd64_stamps", []() {
+    auto t = at::empty({64 * 4 * 8 * 8}, at::kLong);
+    mg::attention_bwd64_stamps(reinterpret_cast<unsigned long long*>(t.data_ptr<int64_t>()));
+    return t;
+  });
+#endif
   m.def("attention_fwd", &attention_fwd);
   m.def("attention_bwd", &attention_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"),
         py::arg("mask"), py::arg("B"), py::arg("T"), py::arg("H"), py::arg("p"), py::arg("seed"),

@@ -113,7 +113,11 @@ void attention_fwd(const bf16_t* qkv, bf16_t* out, float* lse, uint32_t* dmask, 
 // delta [B*H*T] and dq [attention_bwd_workspace_floats] fp32 are workspaces; writes all three
 // slots of dqkv
 size_t attention_bwd_workspace_floats(int B, int T, int H, int hd);
-void attention_set_bwd_mode(int mode);  // 0 auto, 1 persistent (b, h) workgroups, 2 key-block partials
+void attention_set_bwd_mode(int mode);
+void attention_set_bwd64(int on);
+#ifdef MG_BWD64_STAMPS
+void attention_bwd64_stamps(unsigned long long* host);  // diagnostic build only
+#endif  // 1 (default): hd = 64 key-block backward attn_bwd64_kernel; 0: the general kernel  // 0 auto, 1 persistent (b, h) workgroups, 2 key-block partials
 // dbias (fp32 [3D] or null): += the column sums of dqkv (the qkv bias gradient), fused into the
 // backward kernels where the schedule allows
 void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const float* lse,

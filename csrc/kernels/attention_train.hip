@@ -30,6 +30,8 @@
 //  * P is converted to bf16 in registers and used directly as the B operand of O^T = V^T P^T;
 //    V^T fragments come from LDS with ds_read_b64_tr_b16 in the matching permuted key order.
 //  * heaviest (last) query blocks are launched first; fully-masked K tiles are skipped per wave.
+#include <type_traits>
+
 #include "attn_common.h"
 #include "kernels.h"
 
@@ -106,6 +108,19 @@ MG_DEVICE void bwd_softmax_grad(f32x16& s, f32x16& dp, const float (&dl)[16], co
     dp[r] = __builtin_fmaf(pd[0], dp[r], -(p[0] * dl[r]));
     dp[r + 1] = __builtin_fmaf(pd[1], dp[r + 1], -(p[1] * dl[r + 1]));
   }
+}
+
+// Row r of bwd_softmax_grad<false> (attn_bwd64_kernel's pinned schedule puts one beside each
+// MFMA); the same operations, so the same results.
+MG_DEVICE void bwd_softmax_one(f32x16& s, f32x16& dp, const float (&dl)[16], const uint32_t (&mwr)[16],
+                               int mw_bit, int r) {
+  const float p = fexp2(s[r]);
+  // v_bfe_i32 through the builtin: an asm statement here cost an s_nop per element (hipcc pads
+  // one state after every asm before a VALU reading its output)
+  const int keep = __builtin_amdgcn_sbfe((int)mwr[r], mw_bit, 1);
+  const float pd = __int_as_float(__float_as_int(p) & keep);
+  s[r] = pd;
+  dp[r] = __builtin_fmaf(pd, dp[r], -(p * dl[r]));
 }
 
 // Staging of a [ROWS][NH * 64] bf16 tile (columns >= hd zero) into NH 64-column LDS images.
@@ -581,6 +596,518 @@ __global__ __launch_bounds__(64 * KW, 1) void attn_bwd_kernel(const AttnArgs a) 
   }
 }
 
+// S / dP~ MFMAs of attn_bwd64_kernel, pinned to VGPR accumulators (the softmax gradient reads them
+// with VALU; hipcc's own choice at this register budget was the accumulator file plus a
+// v_accvgpr_read per element).  hipcc neither pads nor orders inside these statements, so the
+// hazards are handled here: the first MFMA of a chain waits 2 states for a VALU-written C, and the
+// chain's result is first read by VALU a whole stage later (attn_bwd64_kernel's pinned schedule
+// puts 8 dV / dK MFMAs between the chain's end and that read; tests/test_isa_hazards.py checks).
+MG_DEVICE void mfma_v_init(f32x16& acc, const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=v"(acc) : "v"(a), "a"(b), "v"(c));
+}
+MG_DEVICE void mfma_v_zero(f32x16& acc, const bf16x8& a, const bf16x8& b) {  // C = 0
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=v"(acc) : "v"(a), "a"(b));
+}
+MG_DEVICE void mfma_v(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b));
+}
+// An MFMA reads its C operand late: a register it takes as C (the chain's initial S) must not be
+// rewritten for ~11 wait states -- keep_live extends the value's live range to a later point.
+MG_DEVICE void keep_live(const f32x16& v) { asm volatile("" ::"v"(v)); }
+
+#ifdef MG_BWD64_STAMPS
+// Diagnostic build only (-DMG_BWD64_STAMPS): s_memtime per wave at 8 points of each tile of the
+// first 64 workgroups (bench/dev/bwd64_stamps.py reads them back).  Nothing else reads this buffer.
+__device__ unsigned long long g_bwd64_stamps[64 * 4 * 8 * 8];
+#define BWD64_STAMP(tile, pt)                                                                      \
+  do {                                                                                             \
+    if (blockIdx.x < 64 && (tile) < 8 && (threadIdx.x & 63) == 0)                                  \
+      g_bwd64_stamps[((blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (tile)) * 8 + (pt)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define BWD64_STAMP(tile, pt) \
+  do {                        \
+  } while (0)
+#endif
+
+// One LDS-DMA dword per lane (64 consecutive dwords at LDS byte address lds, a wave-uniform value)
+// from a buffer: inline asm so that hipcc neither counts it (it would put vmcnt(0) in front of every
+// later LDS read it cannot tell apart from the DMA's writes) nor keeps a register for it.  M0 is
+// saved and restored inside the statement; the completion is waited for by the caller.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+// kv_rsrc's descriptor as four scalar words (what an asm operand can take)
+MG_DEVICE u32x4_t kv_rsrc_words(const void* base, uint64_t total, uint64_t off) {
+  const uint64_t p = reinterpret_cast<uint64_t>(base) + off;
+  const uint64_t left = off < total ? total - off : 0;
+  u32x4_t d;
+  d[0] = __builtin_amdgcn_readfirstlane((uint32_t)p);
+  d[1] = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32) & 0xffffu);
+  d[2] = __builtin_amdgcn_readfirstlane((uint32_t)(left < 0xffffffffull ? left : 0xffffffffull));
+  d[3] = 0x00020000u;
+  return d;
+}
+MG_DEVICE void dma_dwordx4(const u32x4_t& rs, uint32_t voff, uint32_t soff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(lds), "s"(soff)
+      : "memory");
+}
+MG_DEVICE void dma_dword(const u32x4_t& rs, uint32_t voff, uint32_t soff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dword %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(lds), "s"(soff)
+      : "memory");
+}
+
+// =================================================================== backward, head dim 64
+// Key-block backward for hd = 64 (every GPT-2 size), one wave per SIMD.  Same grid, LDS images,
+// dQ partials and finalize as attn_bwd_kernel<4, 8, false>, and the same arithmetic in the same
+// order (its outputs are bitwise those of that kernel), but organised for instruction-level
+// parallelism inside the wave instead of a second wave per SIMD:
+//  * 4 waves x 64 keys: wave w owns key groups 2w and 2w + 1 (32 keys each, key on the lane).  A
+//    "unit" is one 32-query subtile x one key group: S and dP~ (8 MFMAs), the softmax gradient
+//    (VALU), dV^T / dK^T (8 MFMAs), its dS^T into LDS.  The two groups of a subtile share its Q / dO
+//    row fragments (S / dP~ A operands) and its transposed dO^T / Q^T fragments (dV / dK A operands),
+//    so each is read from LDS once per two units; the groups' K and V rows stay in registers.
+//  * software pipeline over the 8 units of a 128-query tile: unit u+1's S / dP~ MFMAs are issued
+//    beside unit u's softmax-gradient VALU (two accumulator pairs), so the matrix pipe works while
+//    the vector pipe does; the whole tile is one basic block (no per-unit branches).
+//  * the causal mask is folded into the S accumulator's initial value (-lse, or -inf where the key
+//    follows the query): exp2 gives exactly 0 there, so masked, skipped and diagonal units all run
+//    the same straight-line code; only diagonal tiles (some key of the block after some query of
+//    the tile) pay the per-element select, in a second instance of the tile body.  Rows past T
+//    carry -inf from staging.
+//  * every LDS address is a per-lane base computed once per kernel plus an immediate.
+// Register budget: dK^T / dV^T of 2 groups (128), K / V fragments (64), two S / dP~ pairs (64), the
+// next tile's staged Q / dO (32), row constants of two subtiles (64), operand fragments.
+__global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
+  constexpr int BQ = 128, KB = 256, NT = 256, NKS = 4, NO = 2, KW = 8;
+  constexpr int HQ = BQ * ROWB;
+  constexpr int OFF_Q = 0, OFF_DO = HQ, OFF_K = 2 * HQ, OFF_DS = OFF_K + KB * ROWB;
+  constexpr int OFF_L = OFF_DS + 2 * KB * ROWB, OFF_MW = OFF_L + 2 * BQ * 4;
+  constexpr int MWB = KW * BQ * 4;  // one tile's keep words; two buffers (tile parity)
+  constexpr int OFF_DO2 = OFF_MW + 2 * MWB;  // dO image of odd tiles (even tiles: OFF_DO)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h32 = lane >> 5, l32 = lane & 31;
+  const int BH = a.B * a.H;
+  const int bh = blockIdx.x % BH, kb = blockIdx.x / BH;
+  const int b = bh / a.H, hh = bh % a.H;
+  const long ld = 3L * a.D;
+  const bf16_t* Qg = a.qkv + (long)b * a.T * ld + hh * 64;
+  const bf16_t* Kg = Qg + a.D;
+  const bf16_t* Vg = Qg + 2 * a.D;
+  const bf16_t* dOg = a.dout + (long)b * a.T * a.D + hh * 64;
+  const float* lseg = a.lse + (long)bh * a.T;
+  const float* dlg = a.delta + (long)bh * a.T;
+  const int kb0 = kb * KB;
+  const int ntw = 2 * ((a.T + 63) / 64);
+  const int nqt = (a.T + BQ - 1) / BQ;
+  const int t0w = (kb0 / 64) * 2;
+
+  char* const sQ = smem + OFF_Q;
+  char* const sK = smem + OFF_K;
+  char* const sdS = smem + OFF_DS;
+  using stq = Stager<BQ, 1, NT>;
+  using stk = Stager<KB, 1, NT>;
+
+  {  // K <- c K into the LDS image (dQ's B operand; the fragments below come from it)
+    uint4 rk[stk::N];
+    stk::load(rk, Kg, ld, kb0, a.T, 64);
+#pragma unroll
+    for (int i = 0; i < stk::N; ++i) {
+      float f[8];
+      unpack8(rk[i], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= a.scale_log2;
+      rk[i] = pack8(f);
+    }
+    stk::store(sK, rk);
+  }
+  int mykey[2];
+  bf16x8 vf[2][NKS];  // this wave's V rows (dP~'s B operand), group g = keys 64 w + 32 g + lane
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    mykey[g] = kb0 + 64 * w + 32 * g + l32;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const bool ok = mykey[g] < a.T;
+      vf[g][ks] = __builtin_bit_cast(bf16x8, ok ? ld16(Vg + (long)mykey[g] * ld + ks * 16 + 8 * h32) : make_uint4(0, 0, 0, 0));
+    }
+  }
+  // dropout: both groups read the same keep word of a row (the 64-key tile of keys 64 w..), the
+  // second group's bit 8 above the first's (attn_dropmask_kernel layout)
+  const int mw_col = 2 * w + ((l32 >> 2) & 1);
+  const int mw_bit0 = drop_bit((l32 & 3) | (((l32 >> 3) & 3) << 2));
+
+  // ---- per-lane LDS offsets, computed once (every access below adds an immediate)
+  int ro[NKS];  // row-fragment reads (Q, dO, K): row l32, chunk 2 ks + h32
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) ro[ks] = lds_off(l32, (2 * ks + h32) & 7);
+  // transposed reads (dO^T / Q^T): rows 4 h32 + trq (ta) and 8 more (tb), columns trc (+ 32 n).
+  // With tr_off's swizzle, column + 32 flips bit 6 of the offset and row + 8 flips it again and
+  // adds 1024: ta[0] = ta0, ta[1] = ta0 ^ 64, tb[0] = ta[1] + 1024, tb[1] = ta0 + 1024 (two
+  // registers; the 1024 lands in the instruction's offset field)
+  const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+  const int ta0 = tr_off(4 * h32 + trq, trc), ta0x = ta0 ^ 64;
+  // dS^T image writes: key row 64 w + l32 (+ 32 g), query chunk j at wbase + ((16 j) ^ wsw) (two
+  // registers and one v_xad per write instead of 8 offsets held across the tile loop)
+  const int wbase = 64 * w * ROWB + l32 * ROWB + 8 * h32, wsw = swz(l32) << 4;
+  const int rowL = OFF_L + 16 * h32;                     // + 4 (32 qs + 8 g')
+  const int rowMW0 = OFF_MW + 4 * (mw_col * BQ + 4 * h32);  // + 4 (32 qs + 8 g'), + MWB on odd tiles
+
+  f32x16 dk[2][NO], dv[2][NO];
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int n = 0; n < NO; ++n) {
+      dk[g][n] = f32x16{0};
+      dv[g][n] = f32x16{0};
+    }
+  const int qt0 = kb0 / BQ;
+
+  // ---- next-tile staging, in registers (the LDS has no room for a second Q / dO image).  Every
+  // load goes through a descriptor with ONE per-lane base offset; the chunk and tile parts ride in
+  // the scalar offset.  (Per-chunk offset registers were spilled, and each reload's vmcnt(0) put
+  // the tile's loads behind one another: 13k cycles per tile.)
+  // (per-lane offsets recomputed inside issue / commit from an opaque thread id: kept live across
+  // the tile loop they were spilled too)
+  uint4 rq[4];  // Q, chunk c: tile row t / 8 + 32 c, 16-byte chunk t % 8 (dO goes by LDS-DMA)
+  const uint64_t q_total = (uint64_t)a.B * a.T * ld * 2, do_total = (uint64_t)a.B * a.T * a.D * 2;
+  const uint64_t q_org = (uint64_t)((const char*)Qg - (const char*)a.qkv);
+  const uint64_t do_org = (uint64_t)((const char*)dOg - (const char*)a.dout);
+  // keep words: word row t0w + j (j = t / 128 + 2 i), query row q of the tile, DMA'd to LDS as
+  // they are (a word of a row past T or of keys past T meets p = 0 in the softmax -- the -inf rows
+  // and the causal mask -- so its value never matters; reads past this (b, h)'s words return 0 by
+  // the descriptor extent).  Without dropout the LDS words are set to all-ones once.
+  const u32x4_t mw_rs = kv_rsrc_words(a.thr ? a.dmask : nullptr, a.thr ? (uint64_t)(bh + 1) * ntw * a.T * 4 : 0,
+                                      a.thr ? (uint64_t)bh * ntw * a.T * 4 : 0);
+  float rl_raw = 0.f;
+  // row constants: waves 0-1 load lse, waves 2-3 delta (threads [0, BQ) / [BQ, 2 BQ)); rows past
+  // T read 0 (descriptor extent) and are replaced at commit
+  const __amdgpu_buffer_rsrc_t rs_l = kv_rsrc(reinterpret_cast<const bf16_t*>(w >= 2 ? dlg : lseg), (uint64_t)a.T * 4, 0);
+  auto issue = [&](int qt) {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    if (a.thr) {  // keep words straight into LDS buffer qt & 1, issued first (see commit)
+      const uint32_t vmw = (uint32_t)(((t >> 7) * a.T + (t & (BQ - 1))) * 4);
+      const uint32_t lb = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(smem + OFF_MW + (qt & 1) * MWB + 64 * 4 * (threadIdx.x >> 6)));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        dma_dword(mw_rs, vmw, (uint32_t)(((t0w + 2 * i) * a.T + qt * BQ) * 4), lb + NT * 4 * i);
+    }
+    {  // dO straight into its LDS image for tile qt (buffer qt & 1): 16 pieces of 8 rows x 128 B,
+       // 4 per wave; lane -> (row 8 p + lane / 8, stored chunk lane % 8), the swizzle applied on
+       // the source side (logical chunk = stored ^ swz(row); swz's bit 2 follows the piece parity)
+      const u32x4_t rsd = kv_rsrc_words(a.dout, do_total, do_org + (uint64_t)qt * BQ * a.D * 2);
+      const int ln = t & 63, r8 = ln >> 3;
+      const uint32_t v0 = (uint32_t)(r8 * a.D * 2 + (((ln & 7) ^ swz(r8)) << 4));
+      const uint32_t v1 = (uint32_t)(r8 * a.D * 2 + (((ln & 7) ^ swz(r8 + 8)) << 4));
+      const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      const uint32_t lb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(smem + ((qt & 1) ? OFF_DO2 : OFF_DO));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pc = 4 * wv + i;  // piece: rows 8 pc ..
+        dma_dwordx4(rsd, (i & 1) ? v1 : v0, (uint32_t)(8 * pc * a.D * 2), lb + pc * 1024);
+      }
+    }
+    const uint32_t vq = (uint32_t)((t >> 3) * ld * 2 + (t & 7) * 16);
+    const __amdgpu_buffer_rsrc_t rsq = kv_rsrc(a.qkv, q_total, q_org + (uint64_t)qt * BQ * ld * 2);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      rq[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsq, vq, (int)(c * 32 * ld * 2), 0));
+    rl_raw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_l, (t & (BQ - 1)) * 4, qt * BQ * 4, 0));
+  };
+  auto commit = [&](int qt) {
+    // this wave's DMA'd dO rows and keep words (issued before every load waited for here) have
+    // landed; the barrier after the tile publishes them
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    const int wq = lds_off(t >> 3, t & 7);  // + 32 c rows: an immediate (swizzle period 16 rows)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) *reinterpret_cast<uint4*>(sQ + wq + c * 32 * ROWB) = rq[c];
+    const int ql = qt * BQ + (t & (BQ - 1));
+    // S init = -lse (K holds c K), -inf on rows past T: exp2 gives 0 there; delta' = delta / dscale
+    // (1 / dscale computed here: held across the tile loop it was spilled; times the reciprocal,
+    // not a division, as attn_bwd_kernel does)
+    const float rl = (t & BQ) ? (ql < a.T ? rl_raw * (1.f / a.dscale) : 0.f) : (ql < a.T ? -rl_raw : -INFINITY);
+    reinterpret_cast<float*>(smem + OFF_L)[t] = rl;
+  };
+  if (!a.thr) {  // no dropout: every key kept (both buffers)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) reinterpret_cast<uint32_t*>(smem + OFF_MW)[threadIdx.x + NT * i] = 0xffffffffu;
+  }
+  issue(qt0);
+  commit(qt0);
+  __syncthreads();
+
+  // one 128-query tile; DIAG: some key of the block follows some query of the tile.  The diagonal
+  // tiles (the first two of the block) and the rest run in two loops, each with ONE instance of the
+  // tile body: one body per loop keeps the register assignment of the loop-carried accumulators
+  // fixed (two bodies in one loop made hipcc shuffle them between files at every tile)
+  auto run_tile = [&](int qt, auto diag_tag) {
+    constexpr bool DIAG = decltype(diag_tag)::value;
+    const bool more = qt + 1 < nqt;
+    const int qbase = qt * BQ;
+    const int rowMW = rowMW0 + (qt & 1) * MWB;
+    const char* const sdO = smem + ((qt & 1) ? OFF_DO2 : OFF_DO);  // this tile's dO image
+    BWD64_STAMP(qt - qt0, 0);
+    if (more) issue(qt + 1);
+    BWD64_STAMP(qt - qt0, 1);
+    // one 128-query tile: 8 units (subtile qs = u / 2, key group g = u % 2) in a three-deep
+    // software pipeline.  Stage u (0..8) is 16 slots, each ONE MFMA plus one element of unit u's
+    // softmax gradient (exp, keep select, 2 FMAs: about one MFMA gap of vector issue):
+    //   even slot 2k: MFMA k of unit u+1's S / dP~ chain
+    //   odd slot 2m+1: MFMA m of unit u-1's dV^T / dK^T (its P / dS packed in stage u-1)
+    // plus, each where the registers it overwrites have been read for the last time and a few slots
+    // ahead of its first use: bf16 packs and dS^T writes of unit u, the K-fragment ring, the next
+    // subtile's Q / dO / Q^T / dO^T fragments and row constants, the next chain's initial S.  A
+    // sched_barrier after every slot pins this order (hipcc left alone issued each chain as one
+    // burst and the vector work after it).  The chain's results are first read a stage later.
+    auto tile = [&](auto) {
+      bf16x8 qf[NKS], df[NKS];           // Q / dO row fragments of the chain's subtile
+      bf16x8 kfb[2];                     // K-fragment ring of the chain (S's B operand)
+      bf16x8 atr[NO][2], qtr[NO][2];     // dO^T / Q^T fragments of the dV / dK unit's subtile
+      bf16x8 pf[2], dsf[2];              // that unit's bf16 P / dS, by 16-query step
+      f32x16 sacc[2], dpa[2], sinit;     // S / dP~ of units u (by u & 1); next chain's initial S
+      float dl[16];                      // delta' of the softmax unit's rows
+      uint32_t mwr[16];                  // their keep words
+      auto kfrag = [&](int g, int ks) { return lds_row_at(sK + (64 * w + 32 * g) * ROWB, ro[ks]); };
+      auto ld_qd = [&](int qs, int ks) {
+        qf[ks] = lds_row_at(sQ + qs * 32 * ROWB, ro[ks]);
+        df[ks] = lds_row_at(sdO + qs * 32 * ROWB, ro[ks]);
+      };
+      auto ld_tr = [&](int qs, int st) {
+        const int rb = (qs * 32 + 16 * st) * ROWB;
+#pragma unroll
+        for (int n = 0; n < NO; ++n) {
+          const int oa = n ? ta0x : ta0, ob = n ? ta0 : ta0x;  // tb[n] = ob + 1024
+          atr[n][st] = lds_tr_at(sdO + rb, oa, ob + 1024);
+          qtr[n][st] = lds_tr_at(sQ + rb, oa, ob + 1024);
+        }
+      };
+      auto ld_rows = [&](int qs, int g4) {
+        const float4 y = *reinterpret_cast<const float4*>(smem + rowL + 4 * BQ + 4 * (32 * qs + 8 * g4));
+        dl[4 * g4] = y.x; dl[4 * g4 + 1] = y.y; dl[4 * g4 + 2] = y.z; dl[4 * g4 + 3] = y.w;
+        const uint4 m4 = *reinterpret_cast<const uint4*>(smem + rowMW + 4 * (32 * qs + 8 * g4));
+        mwr[4 * g4] = m4.x; mwr[4 * g4 + 1] = m4.y; mwr[4 * g4 + 2] = m4.z; mwr[4 * g4 + 3] = m4.w;
+      };
+      auto ld_init = [&](int u) {  // -lse of unit u's rows (S' = Q (cK)^T - lse)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const float4 x = *reinterpret_cast<const float4*>(smem + rowL + 4 * (32 * (u >> 1) + 8 * g4));
+          sinit[4 * g4] = x.x; sinit[4 * g4 + 1] = x.y; sinit[4 * g4 + 2] = x.z; sinit[4 * g4 + 3] = x.w;
+        }
+      };
+      auto mask_init = [&](int u) {  // causal: -inf where key 64 w + 32 g + l32 follows the row's query
+        if constexpr (DIAG) {
+          const int dlt = kb0 + 64 * w + 32 * (u & 1) - qbase - 32 * (u >> 1) + l32;
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (dlt > (r & 3) + 8 * (r >> 2) + 4 * h32) sinit[r] = -INFINITY;
+        }
+      };
+      // MFMA k (0..7) of unit u's S / dP~ chain, with the K ring refill it frees
+      auto chain_mfma = [&](int u, int k) {
+        const int g = u & 1, ks = k >> 1;
+        f32x16& sn = sacc[u & 1];
+        f32x16& pn = dpa[u & 1];
+        if (k & 1) {
+          if (k == 1) mfma_v_zero(pn, df[0], vf[g][0]);
+          else mfma_v(pn, df[ks], vf[g][ks]);
+        } else {
+          if (k == 0) mfma_v_init(sn, qf[0], kfb[0], sinit);
+          else mfma_v(sn, qf[ks], kfb[ks & 1]);
+          // the ring slot just read: this chain's fragment ks + 2, else the next chain's ks - 2
+          if (ks < 2) kfb[ks & 1] = kfrag(g, ks + 2);
+          else if (u + 1 < 8) kfb[ks & 1] = kfrag((u + 1) & 1, ks - 2);
+        }
+      };
+      auto dvdk_mfma = [&](int u, int m) {  // MFMA m (0..7) of unit u's dV^T / dK^T
+        const int g = u & 1, st = m >> 2, n = (m >> 1) & 1;
+        if (m & 1) dk[g][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qtr[n][st], dsf[st], dk[g][n], 0, 0, 0);
+        else dv[g][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(atr[n][st], pf[st], dv[g][n], 0, 0, 0);
+      };
+      auto pack = [&](int u, int st) {  // unit u's P / dS rows of 16-query step st, and its dS^T
+        pf[st] = pack_frag(sacc[u & 1], st);
+        dsf[st] = pack_frag(dpa[u & 1], st);
+      };
+      auto ds_write = [&](int u, int st) {  // dS^T image: row = key, 4 queries per 8-byte write
+        const int qs = u >> 1, g = u & 1;
+        char* dsb = sdS + (qs >> 1) * KB * ROWB + 32 * g * ROWB;
+        const uint4 dw = __builtin_bit_cast(uint4, dsf[st]);
+        const int j0 = (qs & 1) * 4 + 2 * st;
+        *reinterpret_cast<uint2*>(dsb + wbase + ((16 * j0) ^ wsw)) = make_uint2(dw.x, dw.y);
+        *reinterpret_cast<uint2*>(dsb + wbase + ((16 * (j0 + 1)) ^ wsw)) = make_uint2(dw.z, dw.w);
+      };
+      // ---- prologue: unit 0's chain alone, and what stage 0 needs
+      kfb[0] = kfrag(0, 0);
+      kfb[1] = kfrag(0, 1);
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) ld_qd(0, ks);
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) ld_rows(0, g4);
+      ld_init(0);
+      mask_init(0);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) chain_mfma(0, k);
+      ld_tr(0, 0);
+      ld_tr(0, 1);
+      ld_init(1);
+      mask_init(1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u <= 8; ++u) {
+        const int qs = u >> 1, g = u & 1;
+        const int bit = mw_bit0 + 8 * g;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          if (j & 1) {
+            if (u >= 1) dvdk_mfma(u - 1, j >> 1);
+          } else if (u + 1 < 8) {
+            chain_mfma(u + 1, j >> 1);
+          }
+          if (u < 8) bwd_softmax_one(sacc[u & 1], dpa[u & 1], dl, mwr, bit, j);
+          // ---- loads and packs placed after their registers' last reads
+          if (j == 2 && u >= 1) ds_write(u - 1, 1);
+          if (j == 3 && u + 1 < 8) keep_live(sinit);  // the chain's C, read late by MFMA 0
+          if (j == 4 && u + 2 < 8) ld_init(u + 2);
+          if (j == 8 && u < 8) pack(u, 0);  // rows 0..7 done; step-0 packs of u-1 consumed (slot 7)
+          if (j == 9 && u + 2 < 8) mask_init(u + 2);
+          if (j == 10 && u < 8) ds_write(u, 0);
+          if (j == 15 && u < 8) pack(u, 1);  // rows 8..15 done; step-1 packs of u-1 consumed (slot 15)
+          // next subtile's Q / dO rows once this stage's chain has read them (unit u+1 = (qs, 1))
+          if (g == 0 && u + 1 < 8 && qs + 1 < 4 && (j & 3) == 2) ld_qd(qs + 1, j >> 2);
+          // next subtile's transposed fragments once unit u-1's dV / dK read them (u starts a subtile)
+          if (g == 0 && u >= 1 && u < 8 && j == 7) ld_tr(qs, 0);
+          if (g == 0 && u >= 1 && u < 8 && j == 15) ld_tr(qs, 1);
+          // next subtile's row constants, 4 rows at a time, once this stage's softmax read them
+          if (g == 1 && u < 7 && (j & 3) == 3) ld_rows(qs + 1, j >> 2);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    };
+    tile(diag_tag);
+    BWD64_STAMP(qt - qt0, 2);
+    __syncthreads();  // dS^T of all 256 keys in LDS
+    BWD64_STAMP(qt - qt0, 3);
+    if (more) commit(qt + 1);  // the dQ products read only dS^T and K
+    BWD64_STAMP(qt - qt0, 4);
+    // dQ[32 queries of subtile w][64] = dS (c K), over the keys that precede some query of it
+    const int q0w = qbase + 32 * w;
+    if (q0w + 31 >= kb0) {
+      // offsets recomputed per tile from an opaque lane id: kept live across the loop they were
+      // spilled (the reload's vmcnt(0) waits for the previous tile's dQ stores)
+      int lo = lane;
+      asm volatile("" : "+v"(lo));
+      const int trq2 = (lo & 15) >> 2, trc2 = 16 * ((lo >> 4) & 1) + 4 * (lo & 3), hh32 = lo >> 5;
+      const int qcol = (w & 1) * 32 + trc2;
+      const int da = tr_off(8 * hh32 + trq2, qcol), db = tr_off(8 * hh32 + 4 + trq2, qcol);
+      const int ka[2] = {tr_off(8 * hh32 + trq2, trc2), tr_off(8 * hh32 + trq2, 32 + trc2)};
+      const int kc[2] = {tr_off(8 * hh32 + 4 + trq2, trc2), tr_off(8 * hh32 + 4 + trq2, 32 + trc2)};
+      f32x16 dq[NO] = {f32x16{0}, f32x16{0}};
+      const char* sdSh = sdS + (w >> 1) * KB * ROWB;
+      const int nk = min(KB / 16, (q0w + 32 - kb0 + 15) >> 4);
+      if (nk == KB / 16) {
+#pragma unroll
+        for (int kk = 0; kk < KB / 16; ++kk) {
+          const bf16x8 af = lds_tr_at(sdSh + kk * 16 * ROWB, da, db);
+#pragma unroll
+          for (int n = 0; n < NO; ++n)
+            dq[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, lds_tr_at(sK + kk * 16 * ROWB, ka[n], kc[n]), dq[n], 0, 0, 0);
+        }
+      } else {
+        for (int kk = 0; kk < nk; ++kk) {
+          const bf16x8 af = lds_tr_at(sdSh + kk * 16 * ROWB, da, db);
+#pragma unroll
+          for (int n = 0; n < NO; ++n)
+            dq[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, lds_tr_at(sK + kk * 16 * ROWB, ka[n], kc[n]), dq[n], 0, 0, 0);
+        }
+      }
+      BWD64_STAMP(qt - qt0, 5);
+      // key-block partial: buffer stores through one descriptor whose extent ends at row T of
+      // this sequence (rows past it are dropped), row offsets in SGPRs
+      const uint64_t org = ((uint64_t)kb * a.dq_part + ((uint64_t)b * a.T + qbase) * a.D + (uint64_t)hh * 64) * 4;
+      const uint64_t end = ((uint64_t)kb * a.dq_part + ((uint64_t)b + 1) * a.T * a.D) * 4;
+      const __amdgpu_buffer_rsrc_t rs = kv_rsrc(reinterpret_cast<const bf16_t*>(a.dq), end, org);
+#pragma unroll
+      for (int n = 0; n < NO; ++n) {
+        const int voff = ((32 * w + 4 * h32) * a.D + n * 32 + l32) * 4;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dq[n][r]), rs, voff, ((r & 3) + 8 * (r >> 2)) * a.D * 4, 0);
+      }
+    }
+    BWD64_STAMP(qt - qt0, 6);
+    __syncthreads();
+    BWD64_STAMP(qt - qt0, 7);
+  };
+  const int qdiag = min(nqt, (kb0 + KB + BQ - 1) / BQ);
+  for (int qt = qt0; qt < qdiag; ++qt) run_tile(qt, std::integral_constant<bool, true>{});
+  for (int qt = qdiag; qt < nqt; ++qt) run_tile(qt, std::integral_constant<bool, false>{});
+
+  // dK (scaled), dV (dropout keep scale folded) -> dqkv K / V slots; lane = key,
+  // d = n*32 + 8*(r>>2) + 4*h32 + (r&3)
+  const float sc = a.scale_log2 * 0.6931471805599453f * a.dscale;  // dscale / sqrt(hd)
+  const float vs = a.thr ? a.dscale : 1.f;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    if (mykey[g] < a.T) {
+      bf16_t* krow = a.dqkv + ((long)b * a.T + mykey[g]) * ld + a.D + hh * 64;
+      bf16_t* vrow = krow + a.D;
+#pragma unroll
+      for (int n = 0; n < NO; ++n)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d = n * 32 + 8 * g4 + 4 * h32;
+          *reinterpret_cast<uint2*>(krow + d) = make_uint2(pack2(dk[g][n][4 * g4] * sc, dk[g][n][4 * g4 + 1] * sc),
+                                                           pack2(dk[g][n][4 * g4 + 2] * sc, dk[g][n][4 * g4 + 3] * sc));
+          *reinterpret_cast<uint2*>(vrow + d) = make_uint2(pack2(dv[g][n][4 * g4] * vs, dv[g][n][4 * g4 + 1] * vs),
+                                                           pack2(dv[g][n][4 * g4 + 2] * vs, dv[g][n][4 * g4 + 3] * vs));
+        }
+    }
+  }
+  if (a.dbias) {
+    // qkv bias gradient, K and V columns (as attn_bwd_kernel, key group 2 w + g in the place of
+    // its wave): keys summed over the lanes, the 8 groups through LDS, one atomic per column
+    constexpr int NV = 32 * NO;
+    float* red = reinterpret_cast<float*>(smem);  // [8 groups][NO][64]
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      float v[NV];
+      const bool kv = mykey[g] < a.T;
+#pragma unroll
+      for (int n = 0; n < NO; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          v[n * 16 + r] = kv ? dk[g][n][r] * sc : 0.f;
+          v[16 * NO + n * 16 + r] = kv ? dv[g][n][r] * vs : 0.f;
+        }
+      tr_reduce32<16, NV, NV>(v, lane);
+#pragma unroll
+      for (int j = 0; j < NO; ++j) red[((2 * w + g) * NO + j) * 64 + lane] = v[j];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < 64 * NO; t += NT) {
+      const int ln = t & 63, j = t >> 6;
+      float s = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < KW; ++ww) s += red[(ww * NO + j) * 64 + ln];
+      const int idx = NO * (ln & 31) + j;
+      const int tk = idx / (16 * NO), n = (idx % (16 * NO)) / 16, r = idx % 16;
+      const int d = n * 32 + 8 * (r >> 2) + 4 * (ln >> 5) + (r & 3);
+      atomicAdd(a.dbias + (1 + tk) * a.D + hh * 64 + d, s);
+    }
+  }
+}
+
 // partial mode: dqkv Q slot = bf16(scale * sum of the dQ partials of key blocks kb <= t / KB)
 __global__ __launch_bounds__(256) void attn_dq_finalize_kernel(const float* __restrict__ dq,
                                                                bf16_t* __restrict__ dqkv, int rows,
@@ -647,8 +1174,35 @@ bool bwd_persistent(int T, int hd) {
   return T <= bwd_keys_per_block(hd);
 }
 
+// hd = 64 key-block backward (attn_bwd64_kernel) unless MINGPT_ATTN_BWD64=0 (tests: the general
+// kernel of the same arithmetic, for a bitwise comparison)
+int g_bwd64 = -1;
+
+bool use_bwd64(const AttnArgs& a) {
+  if (g_bwd64 < 0) {
+    const char* e = getenv("MINGPT_ATTN_BWD64");
+    g_bwd64 = e ? atoi(e) : 0;  // work in progress: off until it beats attn_bwd_kernel (PERF.md round 6)
+  }
+  return g_bwd64 && a.hd == 64 && a.dq_part;
+}
+
+void launch_bwd64(const AttnArgs& a, hipStream_t stream) {
+  constexpr int smem = 3 * 128 * ROWB + 256 * ROWB + 2 * 256 * ROWB + 2 * 128 * 4 + 2 * 8 * 128 * 4;
+  static_assert(smem <= 160 * 1024, "attn_bwd64_kernel LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)attn_bwd64_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  const int nkb = (a.T + 255) / 256;
+  attn_bwd64_kernel<<<a.B * a.H * nkb, 256, smem, stream>>>(a);
+}
+
 template <int NKS, int KW>
 void launch_bwd(const AttnArgs& a, hipStream_t stream) {
+  if constexpr (NKS == 4) {
+    if (use_bwd64(a)) return launch_bwd64(a, stream);
+  }
   constexpr int smem_p = bwd_smem<NKS, KW, true>(), smem_k = bwd_smem<NKS, KW, false>();
   static_assert(smem_p <= 160 * 1024 && smem_k <= 160 * 1024, "attention backward LDS budget");
   static bool attr = false;
@@ -710,6 +1264,14 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
 }
 
 void attention_set_bwd_mode(int mode) { g_bwd_mode = mode; }
+
+void attention_set_bwd64(int on) { g_bwd64 = on; }
+
+#ifdef MG_BWD64_STAMPS
+void attention_bwd64_stamps(unsigned long long* host) {
+  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bwd64_stamps), sizeof(g_bwd64_stamps));
+}
+#endif
 
 size_t attention_bwd_workspace_floats(int B, int T, int H, int hd) {
   const size_t one = (size_t)B * T * H * hd;

@@ -61,10 +61,12 @@ def main():
     body = s[m.end():s.find(".Lfunc_end", m.end())].split("\n")
     # outermost loop: hipcc rotates it, so take the span from the earliest label any later branch
     # jumps back to (at or before the Depth=1 header) to the last such back edge
-    hdr = next(i for i, l in enumerate(body) if "Loop Header: Depth=1" in l)
+    hdrs = [i for i, l in enumerate(body) if "Loop Header: Depth=1" in l]
+    hdr = hdrs[int(opts.get("loop", "0"))]  # --loop=N: the N-th outermost loop of the kernel
     lab = {l.split(":")[0].strip(): i for i, l in enumerate(body) if re.match(r"^\.LBB\w+:", l.strip())}
     start, end = hdr, hdr
-    for i, l in enumerate(body):
+    nxt = min([h for h in hdrs if h > hdr] + [len(body)])
+    for i, l in enumerate(body[:nxt]):
         mm = re.search(r"s_c?branch\w*\s+(\.LBB\w+)", l)
         if mm and i > hdr and lab.get(mm.group(1), 1 << 30) <= hdr:
             start, end = min(start, lab[mm.group(1)]), max(end, i)

@@ -108,3 +108,51 @@ if "--lds" in sys.argv:
         print(f"{name[:80]}: {len(bad)} early reads of asm LDS results")
         for b in bad[:6]:
             print("   line", b[0], b[1][:90])
+
+
+# ---- --operands: VGPR / AGPR operands of inline-asm MFMAs (;;#ASMSTART blocks) written by a VALU
+# instruction (v_mov, v_accvgpr_*, v_cndmask, ...) fewer than 2 wait states before the MFMA reads
+# them (hipcc pads only its own MFMAs; the asm statements open with s_nop where they expect it).
+def anyregs(tok):
+    m = re.match(r"([va])\[(\d+):(\d+)\]", tok)
+    if m:
+        return {(m.group(1), r) for r in range(int(m.group(2)), int(m.group(3)) + 1)}
+    m = re.match(r"([va])(\d+)$", tok)
+    return {(m.group(1), int(m.group(2)))} if m else set()
+
+
+if "--operands" in sys.argv:
+    for m in re.finditer(r"^(_Z\S+):\s*;", s, re.M):
+        name = m.group(1)
+        if filt not in name:
+            continue
+        body = s[m.end():s.find(".Lfunc_end", m.end())].split("\n")
+        hist = []  # (wait-state counter, written registers) of recent VALU instructions
+        ws, in_asm, bad = 0, False, []
+        for k, line in enumerate(body):
+            if ";;#ASMSTART" in line:
+                in_asm = True
+            if ";;#ASMEND" in line:
+                in_asm = False
+            t = line.split(";")[0].strip()
+            if not t or t.startswith(".") or t.startswith("#"):
+                continue
+            op = t.split()[0]
+            ops = [o.strip() for o in t[len(op):].split(",")]
+            if op.startswith("s_nop"):
+                ws += int(ops[0]) + 1
+                continue
+            if op.startswith("v_mfma") and in_asm:
+                srcs = set()
+                for o in ops[1:4]:
+                    srcs |= anyregs(o.split()[0]) if o else set()
+                for w_ws, regs_w, txt in hist:
+                    if ws - w_ws < 2 and regs_w & srcs:
+                        bad.append((k, ws - w_ws, txt, t))
+            if op.startswith("v_") and not op.startswith("v_mfma"):
+                hist.append((ws, anyregs(ops[0].split()[0]) if ops and ops[0] else set(), t))
+                hist = hist[-8:]
+            ws += 1
+        print(f"{name[:80]}: {len(bad)} asm-MFMA operands written < 2 wait states before")
+        for b in bad[:8]:
+            print("   line", b[0], "ws=%d" % b[1], b[2][:60], "->", b[3][:70])

@@ -1,4 +1,6 @@
 """Causal flash attention (csrc/kernels/attention.hip) vs the fp32 PyTorch reference."""
+import os
+
 import pytest
 import torch
 
@@ -25,7 +27,8 @@ def _split(qkv, B, T, H):
     return f(q), f(k), f(v)
 
 
-@pytest.mark.parametrize("B,T,H,hd", [(2, 128, 3, 64), (1, 200, 2, 64), (2, 1024, 2, 64), (2, 256, 4, 32),
+@pytest.mark.parametrize("B,T,H,hd", [(2, 128, 3, 64), (1, 200, 2, 64), (2, 1024, 2, 64), (1, 777, 2, 64),
+                                      (2, 520, 3, 64), (2, 256, 4, 32),
                                       (1, 96, 3, 16), (1, 64, 1, 64), (1, 300, 2, 128), (2, 200, 2, 96),
                                       (1, 520, 2, 80), (1, 130, 2, 48), (1, 200, 3, 8), (1, 777, 1, 24),
                                       (1, 256, 2, 112)])
@@ -74,6 +77,31 @@ def test_attention_bwd_fused_bias_grad(B, T, H, hd, p):
     # per element): ~6 sigma of that rounding noise over the column
     tol = 6e-3 * dqkv.float().pow(2).sum(0).max().item() ** 0.5 + 1e-2
     torch.testing.assert_close(db, ref, atol=tol, rtol=2e-3)
+
+
+@pytest.mark.parametrize("B,T,H,p", [(2, 1024, 2, 0.1), (1, 777, 2, 0.1), (1, 520, 3, 0.0), (3, 1000, 1, 0.1),
+                                     (1, 257, 2, 0.1), (2, 2048, 1, 0.1)])
+def test_attention_bwd64_matches_general_kernel(B, T, H, p, bwd_mode):
+    """hd = 64 key-block backward (attn_bwd64_kernel: one wave per SIMD, pipelined units, causal mask
+    in the accumulator init) against the general kernel it replaces (attn_bwd_kernel<4, 8>): the
+    same products in the same order, so dQ / dK / dV agree bitwise; the fused qkv bias gradient up
+    to the order of its cross-workgroup atomics."""
+    C = ext()
+    torch.manual_seed(3)
+    D = H * 64
+    qkv = torch.randn(B * T, 3 * D, device=DEV).to(torch.bfloat16)
+    out, lse, mask = C.attention_fwd(qkv, B, T, H, p, 11)
+    dout = torch.randn(B * T, D, device=DEV).to(torch.bfloat16)
+    res = {}
+    try:
+        for on in (1, 0):
+            C.attention_set_bwd64(on)
+            db = torch.zeros(3 * D, device=DEV)
+            res[on] = (C.attention_bwd(qkv, out, dout, lse, mask, B, T, H, p, 11, db), db)
+    finally:
+        C.attention_set_bwd64(int(os.environ.get("MINGPT_ATTN_BWD64", "0")))
+    assert torch.equal(res[1][0], res[0][0])
+    torch.testing.assert_close(res[1][1], res[0][1], atol=1e-3, rtol=1e-4)
 
 
 def test_attention_causality():

@@ -2,6 +2,7 @@
 MFMAs must not be read by compiler-placed code (epilogue reads, spills, copies) before the MFMA
 result is ready -- hipcc cannot see the latency of an asm MFMA (scripts/mfma_hazards.py)."""
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -42,3 +43,35 @@ def test_gemm_asm_lds_reads_waited(tmp_path):
     assert len(lines) > 10, r.stdout
     bad = [l for l in lines if not l.rstrip().endswith(": 0 early reads of asm LDS results")]
     assert not bad, "\n".join(bad)
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_attention_bwd64_asm_mfma_operands(tmp_path):
+    """attn_bwd64_kernel's S / dP~ MFMAs are inline asm (VGPR accumulators): no compiler-placed VALU
+    write of any of their operands may land < 2 wait states before one (hipcc does not pad asm),
+    and its steady tile loop must hold no scratch access."""
+    out = tmp_path / "attn.s"
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=fast", "-fno-slp-vectorize",
+                    "--cuda-device-only", "-S", "-I" + os.path.join(ROOT, "csrc", "include"),
+                    os.path.join(ROOT, "csrc", "kernels", "attention_train.hip"), "-o", str(out)],
+                   check=True, capture_output=True)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "mfma_hazards.py"), str(out), "attn_bwd64",
+                        "--operands"], check=True, capture_output=True, text=True)
+    lines = [l for l in r.stdout.splitlines() if "asm-MFMA operands" in l]
+    assert len(lines) == 1 and lines[0].rstrip().endswith(": 0 asm-MFMA operands written < 2 wait states before"), r.stdout
+    # no scratch access inside the steady tile loop: a spill reload there waits vmcnt(0), i.e. for
+    # the next tile's in-flight loads / DMA and this tile's dQ stores (measured: 2-8k cycles a tile)
+    text = out.read_text()
+    m = re.search(r"^(_Z\S*attn_bwd64_kernel\S*):", text, re.M)
+    body = text[m.end():text.find(".Lfunc_end", m.end())].split("\n")
+    hdrs = [i for i, l in enumerate(body) if "Loop Header: Depth=1" in l]
+    assert len(hdrs) == 2, "expected the diagonal-tile and steady-tile loops"
+    labels = {l.split(":")[0].strip(): i for i, l in enumerate(body) if re.match(r"^\.LBB\w+:", l.strip())}
+    end = max(i for i, l in enumerate(body)
+              if (mm := re.search(r"s_c?branch\w*\s+(\.LBB\w+)", l)) and i > hdrs[1]
+              and labels.get(mm.group(1), 1 << 30) <= hdrs[1])
+    start = min(labels[mm.group(1)] for i, l in enumerate(body)
+                if (mm := re.search(r"s_c?branch\w*\s+(\.LBB\w+)", l)) and hdrs[1] < i <= end
+                and labels.get(mm.group(1), 1 << 30) <= hdrs[1])
+    scratch = [l.strip() for l in body[start:end + 1] if "scratch_" in l]
+    assert not scratch, scratch[:5]
