@@ -10,6 +10,7 @@ import torch
 from mingpt_distributed_amd.ops._ext import ext
 
 C = ext()
+C.attention_set_bwd64(1)
 B, T, H, hd = int(os.environ.get("ATTN_B", "128")), 1024, 12, 64
 D = H * hd
 qkv = torch.randn(B * T, 3 * D, device="cuda").to(torch.bfloat16)
@@ -18,7 +19,9 @@ out, lse, mask = C.attention_fwd(qkv, B, T, H, 0.1, 1)
 for _ in range(4):
     C.attention_bwd(qkv, out, dout, lse, mask, B, T, H, 0.1, 1)
 torch.cuda.synchronize()
-st = C.attention_bwd64_stamps().view(64, 4, 8, 8).double()
+raw = C.attention_bwd64_stamps()
+st = raw[:64 * 4 * 8 * 8].view(64, 4, 8, 8).double()
+pe = raw[64 * 4 * 8 * 8:].view(64, 4, 4, 2).double()
 names = ["issue", "tile body", "barrier 1", "commit", "dQ MFMA", "dQ store", "barrier 2"]
 print("phase cycles (median over workgroups and waves), tiles 0-1 diagonal, 2-7 steady")
 print(f"{'tile':>4s} " + " ".join(f"{n:>10s}" for n in names) + f" {'total':>8s}")
@@ -29,3 +32,10 @@ for t in range(8):
     print(f"{t:4d} " + " ".join(f"{v:10.0f}" for v in med.tolist()) + f" {tot:8.0f}")
 nxt = (st[:, :, 1:, 0] - st[:, :, :-1, 7]).median().item()
 print(f"between tiles (loop overhead): {nxt:.0f}")
+pro = (pe[:, :, 1, 0] - pe[:, :, 0, 0]).median().item()
+loop = (pe[:, :, 2, 0] - pe[:, :, 1, 0]).median().item()
+epi = (pe[:, :, 3, 0] - pe[:, :, 2, 0]).median().item()
+clk = ((pe[:, :, 3, 0] - pe[:, :, 0, 0]) / (pe[:, :, 3, 1] - pe[:, :, 0, 1]) * 0.1).median().item()
+wall = ((pe[:, :, 3, 1] - pe[:, :, 0, 1]) / 100).median().item()
+print(f"workgroup (key block 0): prologue {pro:.0f}, tile loops {loop:.0f}, epilogue {epi:.0f} cycles; "
+      f"{wall:.1f} us at {clk:.2f} GHz")

@@ -110,11 +110,11 @@ MG_DEVICE void bwd_softmax_grad(f32x16& s, f32x16& dp, const float (&dl)[16], co
   }
 }
 
-// Row r of bwd_softmax_grad<false> (attn_bwd64_kernel's pinned schedule puts one beside each
-// MFMA); the same operations, so the same results.
+// Row r of bwd_softmax_grad<false> given p = exp2(S'[r]) (attn_bwd64_kernel's pinned schedule puts
+// one beside each MFMA, with the next row's exp2 issued in the same slot: two independent chains
+// instead of one 5-deep one per slot); the same operations, so the same results.
 MG_DEVICE void bwd_softmax_one(f32x16& s, f32x16& dp, const float (&dl)[16], const uint32_t (&mwr)[16],
-                               int mw_bit, int r) {
-  const float p = fexp2(s[r]);
+                               int mw_bit, int r, float p) {  // p = fexp2(s[r]), computed ahead
   // v_bfe_i32 through the builtin: an asm statement here cost an s_nop per element (hipcc pads
   // one state after every asm before a VALU reading its output)
   const int keep = __builtin_amdgcn_sbfe((int)mwr[r], mw_bit, 1);
@@ -619,12 +619,25 @@ MG_DEVICE void keep_live(const f32x16& v) { asm volatile("" ::"v"(v)); }
 // Diagnostic build only (-DMG_BWD64_STAMPS): s_memtime per wave at 8 points of each tile of the
 // first 64 workgroups (bench/dev/bwd64_stamps.py reads them back).  Nothing else reads this buffer.
 __device__ unsigned long long g_bwd64_stamps[64 * 4 * 8 * 8];
+// per wave: s_memtime and s_memrealtime (100 MHz) at kernel start, before the tile loops, after
+// them, and at the end
+__device__ unsigned long long g_bwd64_pe[64 * 4 * 8];
+#define BWD64_PE(pt)                                                                               \
+  do {                                                                                             \
+    if (blockIdx.x < 64 && (threadIdx.x & 63) == 0) {                                              \
+      g_bwd64_pe[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + 2 * (pt)] = __builtin_amdgcn_s_memtime(); \
+      g_bwd64_pe[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + 2 * (pt) + 1] = __builtin_amdgcn_s_memrealtime(); \
+    }                                                                                              \
+  } while (0)
 #define BWD64_STAMP(tile, pt)                                                                      \
   do {                                                                                             \
     if (blockIdx.x < 64 && (tile) < 8 && (threadIdx.x & 63) == 0)                                  \
       g_bwd64_stamps[((blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (tile)) * 8 + (pt)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
+#define BWD64_PE(pt) \
+  do {               \
+  } while (0)
 #define BWD64_STAMP(tile, pt) \
   do {                        \
   } while (0)
@@ -687,6 +700,7 @@ MG_DEVICE void dma_dword(const u32x4_t& rs, uint32_t voff, uint32_t soff, uint32
 // Register budget: dK^T / dV^T of 2 groups (128), K / V fragments (64), two S / dP~ pairs (64), the
 // next tile's staged Q / dO (32), row constants of two subtiles (64), operand fragments.
 __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
+  BWD64_PE(0);
   constexpr int BQ = 128, KB = 256, NT = 256, NKS = 4, NO = 2, KW = 8;
   constexpr int HQ = BQ * ROWB;
   constexpr int OFF_Q = 0, OFF_DO = HQ, OFF_K = 2 * HQ, OFF_DS = OFF_K + KB * ROWB;
@@ -716,19 +730,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
   using stq = Stager<BQ, 1, NT>;
   using stk = Stager<KB, 1, NT>;
 
-  {  // K <- c K into the LDS image (dQ's B operand; the fragments below come from it)
-    uint4 rk[stk::N];
-    stk::load(rk, Kg, ld, kb0, a.T, 64);
-#pragma unroll
-    for (int i = 0; i < stk::N; ++i) {
-      float f[8];
-      unpack8(rk[i], f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] *= a.scale_log2;
-      rk[i] = pack8(f);
-    }
-    stk::store(sK, rk);
-  }
+  // prologue loads all issued together, waited for once: K rows (scaled into the LDS image
+  // below), this wave's V rows, then the first tile's Q / dO / row constants / keep words (issue)
+  uint4 rk[stk::N];
+  stk::load(rk, Kg, ld, kb0, a.T, 64);
   int mykey[2];
   bf16x8 vf[2][NKS];  // this wave's V rows (dP~'s B operand), group g = keys 64 w + 32 g + lane
 #pragma unroll
@@ -845,6 +850,16 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
     for (int i = 0; i < 8; ++i) reinterpret_cast<uint32_t*>(smem + OFF_MW)[threadIdx.x + NT * i] = 0xffffffffu;
   }
   issue(qt0);
+  // K <- c K into the LDS image (dQ's B operand; the K fragments of the chains come from it)
+#pragma unroll
+  for (int i = 0; i < stk::N; ++i) {
+    float f[8];
+    unpack8(rk[i], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] *= a.scale_log2;
+    rk[i] = pack8(f);
+  }
+  stk::store(sK, rk);
   commit(qt0);
   __syncthreads();
 
@@ -963,6 +978,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
       ld_init(1);
       mask_init(1);
       __builtin_amdgcn_sched_barrier(0);
+      float pcur = 0.f, pnext = 0.f;  // exp2 of the softmax element of this slot / the next
 #pragma unroll
       for (int u = 0; u <= 8; ++u) {
         const int qs = u >> 1, g = u & 1;
@@ -974,7 +990,12 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
           } else if (u + 1 < 8) {
             chain_mfma(u + 1, j >> 1);
           }
-          if (u < 8) bwd_softmax_one(sacc[u & 1], dpa[u & 1], dl, mwr, bit, j);
+          if (u < 8) {
+            if (j == 0) pcur = fexp2(sacc[u & 1][0]);
+            if (j < 15) pnext = fexp2(sacc[u & 1][j + 1]);
+            bwd_softmax_one(sacc[u & 1], dpa[u & 1], dl, mwr, bit, j, pcur);
+            pcur = pnext;
+          }
           // ---- loads and packs placed after their registers' last reads
           if (j == 2 && u >= 1) ds_write(u - 1, 1);
           if (j == 3 && u + 1 < 8) keep_live(sinit);  // the chain's C, read late by MFMA 0
@@ -1014,21 +1035,29 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
       const int kc[2] = {tr_off(8 * hh32 + 4 + trq2, trc2), tr_off(8 * hh32 + 4 + trq2, 32 + trc2)};
       f32x16 dq[NO] = {f32x16{0}, f32x16{0}};
       const char* sdSh = sdS + (w >> 1) * KB * ROWB;
-      const int nk = min(KB / 16, (q0w + 32 - kb0 + 15) >> 4);
-      if (nk == KB / 16) {
+      {
+        // all 16 key steps, also on diagonal tiles (the steps past the subtile's last query add
+        // exact zeros; a trimmed loop of runtime length measured slower).  The fragments of step
+        // kk + 4 are read while step kk's two MFMAs run (a 4-deep register ring, order pinned;
+        // hipcc left alone read 4 steps, waited, ran their 8 MFMAs, then read the next 4 -- the
+        // LDS latency exposed every 4 steps: 2.8k -> 1.9k cycles per tile)
+        constexpr int R = 4;
+        bf16x8 fa[R], fb[R][NO];
+        auto ld_step = [&](int kk) {
+          fa[kk % R] = lds_tr_at(sdSh + kk * 16 * ROWB, da, db);
+#pragma unroll
+          for (int n = 0; n < NO; ++n) fb[kk % R][n] = lds_tr_at(sK + kk * 16 * ROWB, ka[n], kc[n]);
+        };
+#pragma unroll
+        for (int kk = 0; kk < R; ++kk) ld_step(kk);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int kk = 0; kk < KB / 16; ++kk) {
-          const bf16x8 af = lds_tr_at(sdSh + kk * 16 * ROWB, da, db);
 #pragma unroll
           for (int n = 0; n < NO; ++n)
-            dq[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, lds_tr_at(sK + kk * 16 * ROWB, ka[n], kc[n]), dq[n], 0, 0, 0);
-        }
-      } else {
-        for (int kk = 0; kk < nk; ++kk) {
-          const bf16x8 af = lds_tr_at(sdSh + kk * 16 * ROWB, da, db);
-#pragma unroll
-          for (int n = 0; n < NO; ++n)
-            dq[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, lds_tr_at(sK + kk * 16 * ROWB, ka[n], kc[n]), dq[n], 0, 0, 0);
+            dq[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[kk % R], fb[kk % R][n], dq[n], 0, 0, 0);
+          if (kk + R < KB / 16) ld_step(kk + R);
+          __builtin_amdgcn_sched_barrier(0);
         }
       }
       BWD64_STAMP(qt - qt0, 5);
@@ -1050,28 +1079,38 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
     BWD64_STAMP(qt - qt0, 7);
   };
   const int qdiag = min(nqt, (kb0 + KB + BQ - 1) / BQ);
+  BWD64_PE(1);
   for (int qt = qt0; qt < qdiag; ++qt) run_tile(qt, std::integral_constant<bool, true>{});
   for (int qt = qdiag; qt < nqt; ++qt) run_tile(qt, std::integral_constant<bool, false>{});
+  BWD64_PE(2);
 
   // dK (scaled), dV (dropout keep scale folded) -> dqkv K / V slots; lane = key,
   // d = n*32 + 8*(r>>2) + 4*h32 + (r&3)
   const float sc = a.scale_log2 * 0.6931471805599453f * a.dscale;  // dscale / sqrt(hd)
   const float vs = a.thr ? a.dscale : 1.f;
+  // 16-byte stores (T21): the lanes l32 and l32 + 32 hold interleaved 4-column pieces of one key
+  // row; one v_permlane32_swap per dword gives each the 8 contiguous columns of a 16-column step
+  // (lanes < 32: columns 16 k .. + 7, the others 16 k + 8 .. + 15): half the store instructions
+  // of the row-per-lane 8-byte form, which was store-issue bound
+  auto store_row = [&](bf16_t* row, const f32x16 (&acc)[NO], float scale) {
+#pragma unroll
+    for (int n = 0; n < NO; ++n)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const f32x16& c = acc[n];
+        const uint32_t x0 = pack2(c[8 * k] * scale, c[8 * k + 1] * scale), x1 = pack2(c[8 * k + 2] * scale, c[8 * k + 3] * scale);
+        const uint32_t y0 = pack2(c[8 * k + 4] * scale, c[8 * k + 5] * scale), y1 = pack2(c[8 * k + 6] * scale, c[8 * k + 7] * scale);
+        const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+        const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+        *reinterpret_cast<uint4*>(row + n * 32 + 16 * k + 8 * h32) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      }
+  };
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
-    if (mykey[g] < a.T) {
+    if (mykey[g] < a.T) {  // the same for both lanes of a row: the swaps pair active lanes only
       bf16_t* krow = a.dqkv + ((long)b * a.T + mykey[g]) * ld + a.D + hh * 64;
-      bf16_t* vrow = krow + a.D;
-#pragma unroll
-      for (int n = 0; n < NO; ++n)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int d = n * 32 + 8 * g4 + 4 * h32;
-          *reinterpret_cast<uint2*>(krow + d) = make_uint2(pack2(dk[g][n][4 * g4] * sc, dk[g][n][4 * g4 + 1] * sc),
-                                                           pack2(dk[g][n][4 * g4 + 2] * sc, dk[g][n][4 * g4 + 3] * sc));
-          *reinterpret_cast<uint2*>(vrow + d) = make_uint2(pack2(dv[g][n][4 * g4] * vs, dv[g][n][4 * g4 + 1] * vs),
-                                                           pack2(dv[g][n][4 * g4 + 2] * vs, dv[g][n][4 * g4 + 3] * vs));
-        }
+      store_row(krow, dk[g], sc);
+      store_row(krow + a.D, dv[g], vs);
     }
   }
   if (a.dbias) {
@@ -1106,6 +1145,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
       atomicAdd(a.dbias + (1 + tk) * a.D + hh * 64 + d, s);
     }
   }
+  BWD64_PE(3);
 }
 
 // partial mode: dqkv Q slot = bf16(scale * sum of the dQ partials of key blocks kb <= t / KB)
@@ -1181,7 +1221,7 @@ int g_bwd64 = -1;
 bool use_bwd64(const AttnArgs& a) {
   if (g_bwd64 < 0) {
     const char* e = getenv("MINGPT_ATTN_BWD64");
-    g_bwd64 = e ? atoi(e) : 0;  // work in progress: off until it beats attn_bwd_kernel (PERF.md round 6)
+    g_bwd64 = e ? atoi(e) : 1;
   }
   return g_bwd64 && a.hd == 64 && a.dq_part;
 }
@@ -1270,6 +1310,7 @@ void attention_set_bwd64(int on) { g_bwd64 = on; }
 #ifdef MG_BWD64_STAMPS
 void attention_bwd64_stamps(unsigned long long* host) {
   (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bwd64_stamps), sizeof(g_bwd64_stamps));
+  (void)hipMemcpyFromSymbol(host + 64 * 4 * 8 * 8, HIP_SYMBOL(g_bwd64_pe), sizeof(g_bwd64_pe));
 }
 #endif
 

@@ -5,10 +5,12 @@
 set -o pipefail
 cd "$(dirname "$0")/../.."
 TAG=${1:-bwd64}; R=${2:-2}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
-timeout -k 10 300 python -u -m pytest tests/test_attention_gpu.py -x -q --timeout 120 --timeout-method thread \
-  > "$OUT/attn_tests.log" 2>&1 || { tail -30 "$OUT/attn_tests.log"; exit 1; }
-tail -2 "$OUT/attn_tests.log"
+for on in 1 0; do  # default (bwd64) and the general kernel it replaces
+  MINGPT_ATTN_BWD64=$on timeout -k 10 300 python -u -m pytest tests/test_attention_gpu.py -x -q --timeout 120 \
+    --timeout-method thread > "$OUT/attn_tests_$on.log" 2>&1 || { tail -30 "$OUT/attn_tests_$on.log"; exit 1; }
+  tail -1 "$OUT/attn_tests_$on.log"
+done
 timeout -k 10 300 python -u -m pytest tests/test_dropout_grad_gpu.py -x -v -s --timeout 200 --timeout-method thread \
   > "$OUT/dgrad_tests.log" 2>&1 || { tail -30 "$OUT/dgrad_tests.log"; exit 1; }
 tail -2 "$OUT/dgrad_tests.log"
-bash scripts/gpu/so_attn_stats.sh "$TAG/ab" "$R" tree tree@MINGPT_ATTN_BWD64=0
+bash scripts/gpu/so_attn_stats.sh "$TAG/ab" "$R" tree@MINGPT_ATTN_BWD64=1 tree@MINGPT_ATTN_BWD64=0

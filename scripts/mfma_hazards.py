@@ -112,7 +112,8 @@ if "--lds" in sys.argv:
 
 # ---- --operands: VGPR / AGPR operands of inline-asm MFMAs (;;#ASMSTART blocks) written by a VALU
 # instruction (v_mov, v_accvgpr_*, v_cndmask, ...) fewer than 2 wait states before the MFMA reads
-# them (hipcc pads only its own MFMAs; the asm statements open with s_nop where they expect it).
+# them, and their results read by a non-MFMA instruction fewer than 12 wait states after (hipcc
+# pads only its own MFMAs; the asm statements open with s_nop where they expect it).
 def anyregs(tok):
     m = re.match(r"([va])\[(\d+):(\d+)\]", tok)
     if m:
@@ -128,6 +129,7 @@ if "--operands" in sys.argv:
             continue
         body = s[m.end():s.find(".Lfunc_end", m.end())].split("\n")
         hist = []  # (wait-state counter, written registers) of recent VALU instructions
+        dwrite = {}  # register -> (wait-state counter, text) of the asm MFMA that last wrote it
         ws, in_asm, bad = 0, False, []
         for k, line in enumerate(body):
             if ";;#ASMSTART" in line:
@@ -149,10 +151,23 @@ if "--operands" in sys.argv:
                 for w_ws, regs_w, txt in hist:
                     if ws - w_ws < 2 and regs_w & srcs:
                         bad.append((k, ws - w_ws, txt, t))
+                for r in anyregs(ops[0].split()[0]):
+                    dwrite[r] = (ws, t)
+            elif not op.startswith("v_mfma"):
+                # a VGPR result of an asm MFMA read by anything but an MFMA within 12 wait states
+                # (8-pass XDL write -> VALU / memory read; hipcc does not see the asm's latency)
+                reads = set()
+                for o in ops[1:]:
+                    reads |= anyregs(o.split()[0]) if o else set()
+                for r in reads & set(dwrite):
+                    if ws - dwrite[r][0] < 12:
+                        bad.append((k, ws - dwrite[r][0], dwrite[r][1], t))
+                        break
             if op.startswith("v_") and not op.startswith("v_mfma"):
                 hist.append((ws, anyregs(ops[0].split()[0]) if ops and ops[0] else set(), t))
                 hist = hist[-8:]
             ws += 1
-        print(f"{name[:80]}: {len(bad)} asm-MFMA operands written < 2 wait states before")
+        print(f"{name[:80]}: {len(bad)} asm-MFMA operands written < 2 wait states before "
+              "or results read < 12 after")
         for b in bad[:8]:
             print("   line", b[0], "ws=%d" % b[1], b[2][:60], "->", b[3][:70])

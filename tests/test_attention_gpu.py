@@ -99,7 +99,7 @@ def test_attention_bwd64_matches_general_kernel(B, T, H, p, bwd_mode):
             db = torch.zeros(3 * D, device=DEV)
             res[on] = (C.attention_bwd(qkv, out, dout, lse, mask, B, T, H, p, 11, db), db)
     finally:
-        C.attention_set_bwd64(int(os.environ.get("MINGPT_ATTN_BWD64", "0")))
+        C.attention_set_bwd64(int(os.environ.get("MINGPT_ATTN_BWD64", "1")))
     assert torch.equal(res[1][0], res[0][0])
     torch.testing.assert_close(res[1][1], res[0][1], atol=1e-3, rtol=1e-4)
 
