@@ -294,6 +294,20 @@ void f32_to_bf16(const at::Tensor& src, const at::Tensor& dst) {
   mg::f32_to_bf16(fp(src), bp(dst), src.numel(), cur_stream());
 }
 
+void comm_proxy(const at::Tensor& src, const at::Tensor& scratch, double factor, int64_t channels,
+                double gbps) {
+  TORCH_CHECK(src.is_cuda() && scratch.is_cuda() && src.is_contiguous() && scratch.is_contiguous());
+  const int64_t bytes = src.numel() * src.element_size();
+  TORCH_CHECK(scratch.numel() * scratch.element_size() >= bytes, "comm_proxy: scratch too small");
+  TORCH_CHECK(factor >= 0 && factor < 2 && channels > 0 && channels <= 1024 && gbps >= 0);
+  // a timing model: the bucket's 16-byte-aligned interior is moved, < 32 edge bytes are not
+  const uintptr_t p0 = reinterpret_cast<uintptr_t>(src.data_ptr()), pa = (p0 + 15) & ~uintptr_t(15);
+  const long n16 = bytes >= (int64_t)(pa - p0) ? (long)((bytes - (int64_t)(pa - p0)) / 16) : 0;
+  DevGuard g(src.device());
+  mg::comm_proxy(reinterpret_cast<const void*>(pa), scratch.data_ptr(), n16, (long)(factor * n16),
+                 (int)channels, gbps, cur_stream());
+}
+
 // ------------------------------------------------------------------------------- elementwise
 at::Tensor bias_act(const at::Tensor& x, const c10::optional<at::Tensor>& b,
                     const c10::optional<at::Tensor>& pre, int64_t act) {
@@ -687,6 +701,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("step"), py::arg("grad_scale"), py::arg("clip"), py::arg("table_end"),
         py::arg("moment_end"), py::arg("zero_grad") = py::none());
   m.def("f32_to_bf16", &f32_to_bf16);
+  m.def("comm_proxy", &comm_proxy);
   m.def("bias_act", &bias_act);
   m.def("bias_dropout_residual", &bias_dropout_residual);
   m.def("gelu_bwd", &gelu_bwd);

@@ -59,6 +59,9 @@ void adamw_step(const int64_t* chunk_start, const int* chunk_len, const float* c
                 float b1, float b2, float eps, int step, float grad_scale, float clip,
                 hipStream_t stream, float* zero_grad = nullptr);
 void f32_to_bf16(const float* src, bf16_t* dst, long n, hipStream_t stream);
+// one-GPU stand-in for a ring all-reduce's CU occupancy and duration (comm_proxy.hip)
+void comm_proxy(const void* src, void* dst, long n16, long total16, int channels, double gbps,
+                hipStream_t stream);
 
 // gemv.hip (decode-time skinny GEMM, B <= 8 rows; epi 0 none, 1 bias, 2 bias+GELU, 3 bias+residual)
 bool gemv_supported(int B, int K);

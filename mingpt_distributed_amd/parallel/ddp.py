@@ -36,6 +36,8 @@ for one node of 8 MI355X on a point-to-point xGMI mesh:
 * **Communicator**: c10d's RCCL process group by default, or (``comm="rccl"`` /
   ``MINGPT_COMM=rccl``) the engine's own RCCL communicator and comm stream
   (:mod:`.comm`, ``csrc/comm/rccl_comm.cpp``) with the same stream-ordered wait contract.
+  ``comm="proxy"`` (one-rank group only): :mod:`.comm_proxy`'s one-GPU stand-in for an N-rank
+  all-reduce's CU occupancy and duration, for measuring comm/compute CU sharing on one GPU.
 """
 from __future__ import annotations
 
@@ -105,7 +107,14 @@ class DataParallelEngine:
 
         self.comm_backend = comm or comm_backend_default()
         self.native = None
-        if self.active and self.comm_backend == "rccl":
+        self.proxy = None
+        if self.active and self.comm_backend == "proxy":
+            if self.world != 1:
+                raise RuntimeError("comm='proxy' stands in for the ranks of a one-rank group only")
+            from .comm_proxy import CommProxy
+
+            self.proxy = CommProxy(store.device)
+        elif self.active and self.comm_backend == "rccl":
             if store.device.type != "cuda":
                 raise RuntimeError("comm='rccl' needs GPU parameters (RCCL); use c10d for CPU runs")
             self.native = native if native is not None else RcclCommunicator(process_group, store.device)
@@ -203,6 +212,8 @@ class DataParallelEngine:
         """Start the bucket's collective on ``wire`` (default: the bucket's slice in the wire
         dtype, converted now); returns its work handle."""
         wire = self._wire(b) if wire is None else wire
+        if self.proxy is not None:
+            return self.proxy.all_reduce(wire)
         if self.native is not None:
             return self.native.all_reduce(wire)
         return dist.all_reduce(wire, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
@@ -324,7 +335,8 @@ class DataParallelEngine:
                 "bucket_bytes": [(b.end - b.start) * esz for b in self.buckets],
                 "wire_dtype": "bf16" if esz == 2 else "fp32",
                 "collective": self.collective_kind,
-                "comm_backend": "rccl-native" if self.native is not None else "c10d"}
+                "comm_backend": "proxy" if self.proxy is not None else
+                "rccl-native" if self.native is not None else "c10d"}
 
     collective_kind = "all_reduce"
 

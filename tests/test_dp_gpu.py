@@ -290,6 +290,53 @@ def test_gpu_rccl_one_rank_collective_paths(tmp_path, zero1, bf16, comm):
     assert cos > 0.995, cos
 
 
+def _worker_proxy(port, out_dir):
+    """comm="proxy" (parallel/comm_proxy.py) on a one-rank group: each bucket's stand-in kernel
+    runs on its own stream at the bucket-ready point, leaves the gradients alone (the weights
+    match a no-communication engine's), is waited on before the optimizer, and lasts its paced
+    time when alone on the GPU."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MINGPT_PROXY_GBPS="50",
+                      MINGPT_PROXY_CHANNELS="16", MINGPT_PROXY_RANKS="8")
+    import torch.distributed as dist
+
+    from mingpt_distributed_amd.trainer import StepEngine
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    eng = StepEngine(_model(), lr=1e-3, grad_clip=1.0, device=dev, bucket_mb=0.5, comm_at_world1=True,
+                     comm="proxy")
+    ref = StepEngine(_model(), lr=1e-3, grad_clip=1.0, device=dev)
+    proxy = eng.dp.proxy
+    assert proxy is not None and eng.dp.comm_plan()["comm_backend"] == "proxy" and len(eng.dp.buckets) > 3
+    x, y = _batch()
+    proxy.record = True
+    for _ in range(3):
+        eng.train_step([(x.cuda(), y.cuda())])
+        ref.train_step([(x.cuda(), y.cuda())])
+    proxy = eng.dp.proxy  # the engine may have rebuilt its buckets after step 1
+    recs = proxy.take_records()
+    assert recs and all(t > 0 for _, t in recs)
+    a, b = eng.model_state_dict(), ref.model_state_dict()
+    for k in a:  # wte's gradient is an fp32-atomic scatter: Adam may differ by ~lr there
+        assert (a[k] - b[k]).abs().max().item() <= 3.5e-3, k
+    iso = eng.dp.time_collectives(reps=3)
+    for bk, t in zip(eng.dp.buckets, iso):
+        m = proxy.model_ms((bk.end - bk.start) * 4)
+        assert 0.8 * m < t < 1.5 * m + 0.05, (t, m)
+    dist.destroy_process_group()
+
+
+def test_gpu_comm_proxy_one_rank(tmp_path):
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_worker_proxy, args=(_port(), str(tmp_path)))
+    p.start()
+    p.join(timeout=100)
+    if p.is_alive():
+        p.kill()
+    assert p.exitcode == 0, p.exitcode
+
+
 def _worker_nccl2(rank, world, port, out_dir, zero1, comm="c10d"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
