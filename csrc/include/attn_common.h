@@ -35,6 +35,7 @@ struct AttnArgs {
   uint32_t thr;        // 16-bit keep threshold: keep iff a 16-bit uniform >= thr (0 = no dropout)
   float dscale;        // 1 / (1 - thr/65536)
   float* dbias;        // bwd key-block mode: += column sums of dK / dV into [D, 3D) (qkv bias grad), or null
+  int* work;           // bwd hd = 64: work-item counter (zeroed by attn_bwd_pre_kernel)
 };
 
 // 16-column MFMA k-steps a head dim is instantiated with: {1, 2, 3, 4, 6, 8}

@@ -47,11 +47,12 @@ namespace {
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restrict__ dout,
                                                            const bf16_t* __restrict__ out,
                                                            float* __restrict__ delta, int BT, int T,
-                                                           int H, int hd, int lg) {
+                                                           int H, int hd, int lg, int* __restrict__ work) {
   // thread -> (row bt, head h, chunk c < cpr = 2^lg): cpr = chunks per head row rounded up to a
   // power of two; 32-bit index arithmetic (B*T*H*cpr < 2^31 is checked on the host)
   const int cpr = 1 << lg;
   const unsigned i = blockIdx.x * 256u + threadIdx.x;
+  if (i == 0 && work) *work = 0;  // attn_bwd64_kernel's item counter, for the launch after this one
   const int c = (int)(i & (cpr - 1));
   const unsigned rh = i >> lg;
   const int hh = (int)(rh % (unsigned)H);
@@ -624,14 +625,14 @@ __device__ unsigned long long g_bwd64_stamps[64 * 4 * 8 * 8];
 __device__ unsigned long long g_bwd64_pe[64 * 4 * 8];
 #define BWD64_PE(pt)                                                                               \
   do {                                                                                             \
-    if (blockIdx.x < 64 && (threadIdx.x & 63) == 0) {                                              \
+    if (bwd64_first && blockIdx.x < 64 && (threadIdx.x & 63) == 0) {                               \
       g_bwd64_pe[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + 2 * (pt)] = __builtin_amdgcn_s_memtime(); \
       g_bwd64_pe[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + 2 * (pt) + 1] = __builtin_amdgcn_s_memrealtime(); \
     }                                                                                              \
   } while (0)
 #define BWD64_STAMP(tile, pt)                                                                      \
   do {                                                                                             \
-    if (blockIdx.x < 64 && (tile) < 8 && (threadIdx.x & 63) == 0)                                  \
+    if (bwd64_first && blockIdx.x < 64 && (tile) < 8 && (threadIdx.x & 63) == 0)                   \
       g_bwd64_stamps[((blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (tile)) * 8 + (pt)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
@@ -700,6 +701,7 @@ MG_DEVICE void dma_dword(const u32x4_t& rs, uint32_t voff, uint32_t soff, uint32
 // Register budget: dK^T / dV^T of 2 groups (128), K / V fragments (64), two S / dP~ pairs (64), the
 // next tile's staged Q / dO (32), row constants of two subtiles (64), operand fragments.
 __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
+  [[maybe_unused]] bool bwd64_first = true;  // stamps (diagnostic build): the first item only
   BWD64_PE(0);
   constexpr int BQ = 128, KB = 256, NT = 256, NKS = 4, NO = 2, KW = 8;
   constexpr int HQ = BQ * ROWB;
@@ -707,44 +709,84 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
   constexpr int OFF_L = OFF_DS + 2 * KB * ROWB, OFF_MW = OFF_L + 2 * BQ * 4;
   constexpr int MWB = KW * BQ * 4;  // one tile's keep words; two buffers (tile parity)
   constexpr int OFF_DO2 = OFF_MW + 2 * MWB;  // dO image of odd tiles (even tiles: OFF_DO)
+  constexpr int OFF_ITEM = OFF_DO2 + HQ;     // the next work item (one int)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h32 = lane >> 5, l32 = lane & 31;
   const int BH = a.B * a.H;
-  const int bh = blockIdx.x % BH, kb = blockIdx.x / BH;
-  const int b = bh / a.H, hh = bh % a.H;
   const long ld = 3L * a.D;
-  const bf16_t* Qg = a.qkv + (long)b * a.T * ld + hh * 64;
-  const bf16_t* Kg = Qg + a.D;
-  const bf16_t* Vg = Qg + 2 * a.D;
-  const bf16_t* dOg = a.dout + (long)b * a.T * a.D + hh * 64;
-  const float* lseg = a.lse + (long)bh * a.T;
-  const float* dlg = a.delta + (long)bh * a.T;
-  const int kb0 = kb * KB;
   const int ntw = 2 * ((a.T + 63) / 64);
   const int nqt = (a.T + BQ - 1) / BQ;
-  const int t0w = (kb0 / 64) * 2;
+  const int n_items = BH * ((a.T + KB - 1) / KB);
 
   char* const sQ = smem + OFF_Q;
   char* const sK = smem + OFF_K;
   char* const sdS = smem + OFF_DS;
-  using stq = Stager<BQ, 1, NT>;
+  int* const sItem = reinterpret_cast<int*>(smem + OFF_ITEM);
   using stk = Stager<KB, 1, NT>;
 
-  // prologue loads all issued together, waited for once: K rows (scaled into the LDS image
-  // below), this wave's V rows, then the first tile's Q / dO / row constants / keep words (issue)
-  uint4 rk[stk::N];
-  stk::load(rk, Kg, ld, kb0, a.T, 64);
+  // ---- work items: (key block, b, h) = (item / BH, item % BH), heaviest key blocks first.  Each
+  // workgroup takes blockIdx.x, then the next free item from the counter (zeroed by
+  // attn_bwd_pre_kernel): a workgroup that starts late (CUs held by a concurrent kernel) takes
+  // fewer.  The next item is known one item ahead, so its K / V / first-tile loads are issued
+  // under the current item's last tile and epilogue instead of after them.
+  int item = blockIdx.x;
+  int bh, kb, b, hh, kb0, qt0;
   int mykey[2];
-  bf16x8 vf[2][NKS];  // this wave's V rows (dP~'s B operand), group g = keys 64 w + 32 g + lane
+  auto setup = [&](int it) {
+    bh = it % BH;
+    kb = it / BH;
+    b = bh / a.H;
+    hh = bh % a.H;
+    kb0 = kb * KB;
+    qt0 = kb0 / BQ;
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    mykey[g] = kb0 + 64 * w + 32 * g + l32;
+    for (int g = 0; g < 2; ++g) mykey[g] = kb0 + 64 * w + 32 * g + l32;
+  };
+  setup(item);
+
+  // K and V rows of an item, raw, by LDS-DMA into the dS^T image (K at OFF_DS, V 32 KiB on):
+  // 8 rows x 128 B per instruction, 8 per wave each; rows past T read 0 (descriptor extent).  No
+  // registers held while they fly (the next item's are issued before the current epilogue)
+  auto dma_kv = [&](int ib, int ihh, int ikb0) {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    const int ln = t & 63;
+    const uint32_t v0 = (uint32_t)((ln >> 3) * ld * 2 + (ln & 7) * 16);
+    const uint64_t org = (((uint64_t)ib * a.T + ikb0) * ld + a.D + ihh * 64) * 2;
+    const uint64_t ext = (uint64_t)(a.T - ikb0 - 1) * ld * 2 + 128;
+    const u32x4_t rk_ = kv_rsrc_words(a.qkv, org + ext, org), rv_ = kv_rsrc_words(a.qkv, org + ext + a.D * 2, org + a.D * 2);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(smem + OFF_DS);
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      const bool ok = mykey[g] < a.T;
-      vf[g][ks] = __builtin_bit_cast(bf16x8, ok ? ld16(Vg + (long)mykey[g] * ld + ks * 16 + 8 * h32) : make_uint4(0, 0, 0, 0));
+    for (int i = 0; i < 8; ++i) {
+      const int pc = 8 * wv + i;  // rows 8 pc ..
+      dma_dwordx4(rk_, v0, (uint32_t)(8 * pc * ld * 2), lb + pc * 1024);
+      dma_dwordx4(rv_, v0, (uint32_t)(8 * pc * ld * 2), lb + KB * ROWB + pc * 1024);
     }
-  }
+  };
+  bf16x8 vf[2][NKS];  // this wave's V rows (dP~'s B operand), group g = keys 64 w + 32 g + lane
+  // after dma_kv landed (vmcnt(0) + barrier): K <- c K into its LDS image (dQ's B operand; the K
+  // fragments of the chains come from it), this wave's V fragments into registers
+  auto convert_kv = [&]() {
+    uint4 rk[stk::N];
+#pragma unroll
+    for (int i = 0; i < stk::N; ++i) {
+      const int idx = threadIdx.x + NT * i, rem = idx % (KB * 8);
+      rk[i] = *reinterpret_cast<const uint4*>(sdS + (rem >> 3) * ROWB + (rem & 7) * 16);
+      float f[8];
+      unpack8(rk[i], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= a.scale_log2;
+      rk[i] = pack8(f);
+    }
+    stk::store(sK, rk);
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+        vf[g][ks] = *reinterpret_cast<const bf16x8*>(sdS + KB * ROWB + (64 * w + 32 * g + l32) * ROWB + ks * 32 + 16 * h32);
+  };
+  dma_kv(b, hh, kb0);
   // dropout: both groups read the same keep word of a row (the 64-key tile of keys 64 w..), the
   // second group's bit 8 above the first's (attn_dropmask_kernel layout)
   const int mw_col = 2 * w + ((l32 >> 2) & 1);
@@ -767,14 +809,16 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
   const int rowMW0 = OFF_MW + 4 * (mw_col * BQ + 4 * h32);  // + 4 (32 qs + 8 g'), + MWB on odd tiles
 
   f32x16 dk[2][NO], dv[2][NO];
+  auto zero_acc = [&]() {
 #pragma unroll
-  for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < 2; ++g)
 #pragma unroll
-    for (int n = 0; n < NO; ++n) {
-      dk[g][n] = f32x16{0};
-      dv[g][n] = f32x16{0};
-    }
-  const int qt0 = kb0 / BQ;
+      for (int n = 0; n < NO; ++n) {
+        dk[g][n] = f32x16{0};
+        dv[g][n] = f32x16{0};
+      }
+  };
+  zero_acc();
 
   // ---- next-tile staging, in registers (the LDS has no room for a second Q / dO image).  Every
   // load goes through a descriptor with ONE per-lane base offset; the chunk and tile parts ride in
@@ -784,49 +828,51 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
   // the tile loop they were spilled too)
   uint4 rq[4];  // Q, chunk c: tile row t / 8 + 32 c, 16-byte chunk t % 8 (dO goes by LDS-DMA)
   const uint64_t q_total = (uint64_t)a.B * a.T * ld * 2, do_total = (uint64_t)a.B * a.T * a.D * 2;
-  const uint64_t q_org = (uint64_t)((const char*)Qg - (const char*)a.qkv);
-  const uint64_t do_org = (uint64_t)((const char*)dOg - (const char*)a.dout);
-  // keep words: word row t0w + j (j = t / 128 + 2 i), query row q of the tile, DMA'd to LDS as
-  // they are (a word of a row past T or of keys past T meets p = 0 in the softmax -- the -inf rows
-  // and the causal mask -- so its value never matters; reads past this (b, h)'s words return 0 by
-  // the descriptor extent).  Without dropout the LDS words are set to all-ones once.
-  const u32x4_t mw_rs = kv_rsrc_words(a.thr ? a.dmask : nullptr, a.thr ? (uint64_t)(bh + 1) * ntw * a.T * 4 : 0,
-                                      a.thr ? (uint64_t)bh * ntw * a.T * 4 : 0);
   float rl_raw = 0.f;
-  // row constants: waves 0-1 load lse, waves 2-3 delta (threads [0, BQ) / [BQ, 2 BQ)); rows past
-  // T read 0 (descriptor extent) and are replaced at commit
-  const __amdgpu_buffer_rsrc_t rs_l = kv_rsrc(reinterpret_cast<const bf16_t*>(w >= 2 ? dlg : lseg), (uint64_t)a.T * 4, 0);
-  auto issue = [&](int qt) {
+  // tile qt of the current item (bh, kb) into the LDS buffers of parity par.  Keep words: word row
+  // t0w + j (j = t / 128 + 2 i), query row q of the tile, DMA'd to LDS as they are (a word of a row
+  // past T or of keys past T meets p = 0 in the softmax -- the -inf rows and the causal mask -- so
+  // its value never matters; reads past this (b, h)'s words return 0 by the descriptor extent).
+  // Without dropout the LDS words are set to all-ones once.  Row constants: waves 0-1 load lse,
+  // waves 2-3 delta (threads [0, BQ) / [BQ, 2 BQ)); rows past T read 0 (descriptor extent) and
+  // are replaced at commit.
+  auto issue = [&](int ib, int ihh, int ibh, int ikb0, int qt, int par) {
+    const int it0w = (ikb0 / 64) * 2;
     int t = threadIdx.x;
     asm volatile("" : "+v"(t));
-    if (a.thr) {  // keep words straight into LDS buffer qt & 1, issued first (see commit)
+    if (a.thr) {  // keep words straight into LDS buffer par, issued first (see commit)
+      const u32x4_t mw_rs = kv_rsrc_words(a.dmask, (uint64_t)(ibh + 1) * ntw * a.T * 4, (uint64_t)ibh * ntw * a.T * 4);
       const uint32_t vmw = (uint32_t)(((t >> 7) * a.T + (t & (BQ - 1))) * 4);
       const uint32_t lb = __builtin_amdgcn_readfirstlane(
-          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(smem + OFF_MW + (qt & 1) * MWB + 64 * 4 * (threadIdx.x >> 6)));
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(smem + OFF_MW + par * MWB + 64 * 4 * (threadIdx.x >> 6)));
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        dma_dword(mw_rs, vmw, (uint32_t)(((t0w + 2 * i) * a.T + qt * BQ) * 4), lb + NT * 4 * i);
+        dma_dword(mw_rs, vmw, (uint32_t)(((it0w + 2 * i) * a.T + qt * BQ) * 4), lb + NT * 4 * i);
     }
-    {  // dO straight into its LDS image for tile qt (buffer qt & 1): 16 pieces of 8 rows x 128 B,
+    {  // dO straight into its LDS image for tile qt (buffer par): 16 pieces of 8 rows x 128 B,
        // 4 per wave; lane -> (row 8 p + lane / 8, stored chunk lane % 8), the swizzle applied on
        // the source side (logical chunk = stored ^ swz(row); swz's bit 2 follows the piece parity)
+      const uint64_t do_org = ((uint64_t)ib * a.T * a.D + (uint64_t)ihh * 64) * 2;
       const u32x4_t rsd = kv_rsrc_words(a.dout, do_total, do_org + (uint64_t)qt * BQ * a.D * 2);
       const int ln = t & 63, r8 = ln >> 3;
       const uint32_t v0 = (uint32_t)(r8 * a.D * 2 + (((ln & 7) ^ swz(r8)) << 4));
       const uint32_t v1 = (uint32_t)(r8 * a.D * 2 + (((ln & 7) ^ swz(r8 + 8)) << 4));
       const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-      const uint32_t lb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(smem + ((qt & 1) ? OFF_DO2 : OFF_DO));
+      const uint32_t lb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(smem + (par ? OFF_DO2 : OFF_DO));
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int pc = 4 * wv + i;  // piece: rows 8 pc ..
         dma_dwordx4(rsd, (i & 1) ? v1 : v0, (uint32_t)(8 * pc * a.D * 2), lb + pc * 1024);
       }
     }
+    const uint64_t q_org = ((uint64_t)ib * a.T * ld + (uint64_t)ihh * 64) * 2;
     const uint32_t vq = (uint32_t)((t >> 3) * ld * 2 + (t & 7) * 16);
     const __amdgpu_buffer_rsrc_t rsq = kv_rsrc(a.qkv, q_total, q_org + (uint64_t)qt * BQ * ld * 2);
 #pragma unroll
     for (int c = 0; c < 4; ++c)
       rq[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsq, vq, (int)(c * 32 * ld * 2), 0));
+    const __amdgpu_buffer_rsrc_t rs_l = kv_rsrc(reinterpret_cast<const bf16_t*>((w >= 2 ? a.delta : a.lse) + (long)ibh * a.T),
+                                                (uint64_t)a.T * 4, 0);
     rl_raw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_l, (t & (BQ - 1)) * 4, qt * BQ * 4, 0));
   };
   auto commit = [&](int qt) {
@@ -849,20 +895,16 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) reinterpret_cast<uint32_t*>(smem + OFF_MW)[threadIdx.x + NT * i] = 0xffffffffu;
   }
-  issue(qt0);
-  // K <- c K into the LDS image (dQ's B operand; the K fragments of the chains come from it)
-#pragma unroll
-  for (int i = 0; i < stk::N; ++i) {
-    float f[8];
-    unpack8(rk[i], f);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] *= a.scale_log2;
-    rk[i] = pack8(f);
-  }
-  stk::store(sK, rk);
-  commit(qt0);
+  int par = 0;  // LDS buffer parity of the current tile's dO image and keep words
+  issue(b, hh, bh, kb0, qt0, par);
+  if (threadIdx.x == 0) *sItem = atomicAdd(a.work, 1) + (int)gridDim.x;  // the item after this one
+  commit(qt0);  // its vmcnt(0) covers dma_kv
+  __syncthreads();
+  convert_kv();
   __syncthreads();
 
+  int nxt = 0, nbh = 0, nb = 0, nhh = 0, nkb0 = 0;  // the next item (valid if has_next)
+  bool has_next = false;
   // one 128-query tile; DIAG: some key of the block follows some query of the tile.  The diagonal
   // tiles (the first two of the block) and the rest run in two loops, each with ONE instance of the
   // tile body: one body per loop keeps the register assignment of the loop-carried accumulators
@@ -871,10 +913,11 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
     constexpr bool DIAG = decltype(diag_tag)::value;
     const bool more = qt + 1 < nqt;
     const int qbase = qt * BQ;
-    const int rowMW = rowMW0 + (qt & 1) * MWB;
-    const char* const sdO = smem + ((qt & 1) ? OFF_DO2 : OFF_DO);  // this tile's dO image
+    const int rowMW = rowMW0 + par * MWB;
+    const char* const sdO = smem + (par ? OFF_DO2 : OFF_DO);  // this tile's dO image
     BWD64_STAMP(qt - qt0, 0);
-    if (more) issue(qt + 1);
+    const int qn = more ? qt + 1 : nkb0 / BQ;  // the next tile: this item's, or the next item's first
+    if (more || has_next) issue(more ? b : nb, more ? hh : nhh, more ? bh : nbh, more ? kb0 : nkb0, qn, par ^ 1);
     BWD64_STAMP(qt - qt0, 1);
     // one 128-query tile: 8 units (subtile qs = u / 2, key group g = u % 2) in a three-deep
     // software pipeline.  Stage u (0..8) is 16 slots, each ONE MFMA plus one element of unit u's
@@ -1019,7 +1062,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
     BWD64_STAMP(qt - qt0, 2);
     __syncthreads();  // dS^T of all 256 keys in LDS
     BWD64_STAMP(qt - qt0, 3);
-    if (more) commit(qt + 1);  // the dQ products read only dS^T and K
+    if (more || has_next) commit(qn);  // the dQ products read only dS^T and K
     BWD64_STAMP(qt - qt0, 4);
     // dQ[32 queries of subtile w][64] = dS (c K), over the keys that precede some query of it
     const int q0w = qbase + 32 * w;
@@ -1077,12 +1120,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
     BWD64_STAMP(qt - qt0, 6);
     __syncthreads();
     BWD64_STAMP(qt - qt0, 7);
+    par ^= 1;
   };
-  const int qdiag = min(nqt, (kb0 + KB + BQ - 1) / BQ);
-  BWD64_PE(1);
-  for (int qt = qt0; qt < qdiag; ++qt) run_tile(qt, std::integral_constant<bool, true>{});
-  for (int qt = qdiag; qt < nqt; ++qt) run_tile(qt, std::integral_constant<bool, false>{});
-  BWD64_PE(2);
 
   // dK (scaled), dV (dropout keep scale folded) -> dqkv K / V slots; lane = key,
   // d = n*32 + 8*(r>>2) + 4*h32 + (r&3)
@@ -1105,6 +1144,21 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
         *reinterpret_cast<uint4*>(row + n * 32 + 16 * k + 8 * h32) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
       }
   };
+  for (;;) {
+  nxt = __builtin_amdgcn_readfirstlane(*sItem);  // published by the barrier that ended the prologue
+  has_next = nxt < n_items;
+  nbh = nxt % BH;
+  nkb0 = (nxt / BH) * KB;
+  nb = nbh / a.H;
+  nhh = nbh % a.H;
+  const int qdiag = min(nqt, (kb0 + KB + BQ - 1) / BQ);
+  BWD64_PE(1);
+  for (int qt = qt0; qt < qdiag; ++qt) run_tile(qt, std::integral_constant<bool, true>{});
+  for (int qt = qdiag; qt < nqt; ++qt) run_tile(qt, std::integral_constant<bool, false>{});
+  BWD64_PE(2);
+  // the next item's K / V (the dS^T image is free: the last tile's dQ products are behind its
+  // final barrier), under this epilogue's stores
+  if (has_next) dma_kv(nb, nhh, nkb0);
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     if (mykey[g] < a.T) {  // the same for both lanes of a row: the swaps pair active lanes only
@@ -1117,7 +1171,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
     // qkv bias gradient, K and V columns (as attn_bwd_kernel, key group 2 w + g in the place of
     // its wave): keys summed over the lanes, the 8 groups through LDS, one atomic per column
     constexpr int NV = 32 * NO;
-    float* red = reinterpret_cast<float*>(smem);  // [8 groups][NO][64]
+    // [8 groups][NO][64] in the dO buffer the last tile used (the Q image and the other dO buffer
+    // hold the next item's first tile, the dS^T image its K / V)
+    float* red = reinterpret_cast<float*>(smem + (par ? OFF_DO : OFF_DO2));
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
       float v[NV];
@@ -1145,7 +1201,22 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
       atomicAdd(a.dbias + (1 + tk) * a.D + hh * 64 + d, s);
     }
   }
+  // the item after the next one (its atomic's latency under this epilogue's stores); read after
+  // the next item's prologue barrier
+  if (threadIdx.x == 0 && has_next) *sItem = atomicAdd(a.work, 1) + (int)gridDim.x;
   BWD64_PE(3);
+  if (!has_next) break;
+  // ---- the next item's prologue: its first tile was staged by the last tile, its K / V rows
+  // DMA'd under the epilogue
+  item = nxt;
+  setup(item);
+  zero_acc();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  convert_kv();
+  __syncthreads();
+  bwd64_first = false;
+  }
 }
 
 // partial mode: dqkv Q slot = bf16(scale * sum of the dQ partials of key blocks kb <= t / KB)
@@ -1227,15 +1298,25 @@ bool use_bwd64(const AttnArgs& a) {
 }
 
 void launch_bwd64(const AttnArgs& a, hipStream_t stream) {
-  constexpr int smem = 3 * 128 * ROWB + 256 * ROWB + 2 * 256 * ROWB + 2 * 128 * 4 + 2 * 8 * 128 * 4;
+  constexpr int smem = 3 * 128 * ROWB + 256 * ROWB + 2 * 256 * ROWB + 2 * 128 * 4 + 2 * 8 * 128 * 4 + 16;
   static_assert(smem <= 160 * 1024, "attn_bwd64_kernel LDS budget");
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)attn_bwd64_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
-  const int nkb = (a.T + 255) / 256;
-  attn_bwd64_kernel<<<a.B * a.H * nkb, 256, smem, stream>>>(a);
+  // one workgroup per CU (the LDS holds one), each sweeping work items (attn_bwd64_kernel)
+  static int ncu[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (!ncu[dev]) {
+    int n = 0;
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    ncu[dev] = n > 0 ? n : 256;
+  }
+  const int items = a.B * a.H * ((a.T + 255) / 256);
+  attn_bwd64_kernel<<<items < ncu[dev] ? items : ncu[dev], 256, smem, stream>>>(a);
 }
 
 template <int NKS, int KW>
@@ -1285,7 +1366,8 @@ void attention_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, con
   int lg = 0;
   while ((8 << lg) < hd) ++lg;
   const long nthreads = (long)B * T * H << lg;
-  attn_bwd_pre_kernel<<<(unsigned)cdiv(nthreads, 256), 256, 0, stream>>>(dout, out, delta, B * T, T, H, hd, lg);
+  a.work = use_bwd64(a) ? reinterpret_cast<int*>(dq + attention_bwd_workspace_floats(B, T, H, hd) - 64) : nullptr;
+  attn_bwd_pre_kernel<<<(unsigned)cdiv(nthreads, 256), 256, 0, stream>>>(dout, out, delta, B * T, T, H, hd, lg, a.work);
   switch (nks_for(hd)) {
     case 1: launch_bwd<1, 8>(a, stream); break;
     case 2: launch_bwd<2, 8>(a, stream); break;
@@ -1318,7 +1400,7 @@ size_t attention_bwd_workspace_floats(int B, int T, int H, int hd) {
   const size_t one = (size_t)B * T * H * hd;
   if (bwd_persistent(T, hd)) return one;
   const int kb = bwd_keys_per_block(hd);
-  return one * (size_t)((T + kb - 1) / kb);
+  return one * (size_t)((T + kb - 1) / kb) + 64;  // + attn_bwd64_kernel's work counter
 }
 
 }  // namespace mg

@@ -72,12 +72,12 @@ def _to_bf16(src: torch.Tensor, dst: torch.Tensor):
 class DataParallelEngine:
     def __init__(self, store: FlatParamStore, process_group=None, bucket_mb: float = 32.0,
                  reduce_dtype: Optional[torch.dtype] = None, broadcast: bool = True,
-                 comm_at_world1: bool = False, comm: Optional[str] = None, native=None):
+                 comm_at_world1: bool = False, comm: Optional[str] = None, native=None, proxy=None):
         """``comm_at_world1`` runs the collective path even in a one-rank process group (tests
         of the RCCL calls on a one-GPU box); otherwise one rank means no communication.
         ``comm``: ``"c10d"`` or ``"rccl"`` (native communicator; default ``MINGPT_COMM``), GPU
         stores only; ``native``: an existing :class:`~.comm.RcclCommunicator` to reuse (rebuilt
-        engines after a bucket relayout)."""
+        engines after a bucket relayout); ``proxy``: likewise an existing comm proxy."""
         self.store = store
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
@@ -113,7 +113,7 @@ class DataParallelEngine:
                 raise RuntimeError("comm='proxy' stands in for the ranks of a one-rank group only")
             from .comm_proxy import CommProxy
 
-            self.proxy = CommProxy(store.device)
+            self.proxy = proxy if proxy is not None else CommProxy(store.device)
         elif self.active and self.comm_backend == "rccl":
             if store.device.type != "cuda":
                 raise RuntimeError("comm='rccl' needs GPU parameters (RCCL); use c10d for CPU runs")

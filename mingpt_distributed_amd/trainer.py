@@ -139,7 +139,7 @@ class StepEngine:
         native = self.dp.native if self.dp is not None else None  # the communicator outlives the layout
         self.dp = DataParallelEngine(new, bucket_mb=self.bucket_mb, reduce_dtype=self.reduce_dtype,
                                      broadcast=False, comm_at_world1=self.comm_at_world1, comm=self.comm,
-                                     native=native)
+                                     native=native, proxy=self.dp.proxy)
         self.dp.observed = None
         self.dp._recording = None
         self.opt.grad_buffer = self.dp.grad_buffer

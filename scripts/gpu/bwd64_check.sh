@@ -13,4 +13,5 @@ done
 timeout -k 10 300 python -u -m pytest tests/test_dropout_grad_gpu.py -x -v -s --timeout 200 --timeout-method thread \
   > "$OUT/dgrad_tests.log" 2>&1 || { tail -30 "$OUT/dgrad_tests.log"; exit 1; }
 tail -2 "$OUT/dgrad_tests.log"
-bash scripts/gpu/so_attn_stats.sh "$TAG/ab" "$R" tree@MINGPT_ATTN_BWD64=1 tree@MINGPT_ATTN_BWD64=0
+# AB_EXTRA: more builds to time beside the tree (e.g. build/ab/prev/_C.so)
+bash scripts/gpu/so_attn_stats.sh "$TAG/ab" "$R" tree $AB_EXTRA tree@MINGPT_ATTN_BWD64=0

@@ -3,7 +3,8 @@
 
     python scripts/isa_census.py attention_train-hip-amdgcn-amd-amdhsa-gfx950.s attn_bwd_kernelILi4ELi8ELb0E
 
-The loop is the outermost one hipcc marks ``Loop Header: Depth=1`` (the body up to its back edge);
+The loop is the outermost one hipcc marks ``Loop Header: Depth=1`` (the body up to its back edge;
+``--depth=2`` for loops nested once, ``--loop=N`` for the N-th of them);
 within it, code behind the wave-uniform branches that only diagonal / tail tiles take is counted
 separately: ``--cold=<regex>,...`` marks every block holding a matching instruction,
 ``--cold-blocks=<name>,...`` names blocks as ``--blocks`` lists them (label, ``#k`` = the k-th
@@ -61,14 +62,16 @@ def main():
     body = s[m.end():s.find(".Lfunc_end", m.end())].split("\n")
     # outermost loop: hipcc rotates it, so take the span from the earliest label any later branch
     # jumps back to (at or before the Depth=1 header) to the last such back edge
-    hdrs = [i for i, l in enumerate(body) if "Loop Header: Depth=1" in l]
-    hdr = hdrs[int(opts.get("loop", "0"))]  # --loop=N: the N-th outermost loop of the kernel
+    depth = int(opts.get("depth", "1"))  # --depth=2: loops nested once (a persistent kernel's tile loops)
+    hdrs = [i for i, l in enumerate(body) if re.search(r"Loop Header: Depth=%d\b" % depth, l)]
+    hdr = hdrs[int(opts.get("loop", "0"))]  # --loop=N: the N-th loop of that depth
     lab = {l.split(":")[0].strip(): i for i, l in enumerate(body) if re.match(r"^\.LBB\w+:", l.strip())}
     start, end = hdr, hdr
     nxt = min([h for h in hdrs if h > hdr] + [len(body)])
+    prev = max([h for h in hdrs if h < hdr] + [0])  # back edges of an enclosing loop jump before it
     for i, l in enumerate(body[:nxt]):
         mm = re.search(r"s_c?branch\w*\s+(\.LBB\w+)", l)
-        if mm and i > hdr and lab.get(mm.group(1), 1 << 30) <= hdr:
+        if mm and i > hdr and prev < lab.get(mm.group(1), 1 << 30) <= hdr:
             start, end = min(start, lab[mm.group(1)]), max(end, i)
     label = body[hdr].split(":")[0].strip()
     # basic blocks: split at labels and after branches

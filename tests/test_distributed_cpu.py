@@ -223,6 +223,10 @@ def _worker_comm_cpu(port, out_dir):
         DataParallelEngine(store, comm_at_world1=True, comm="rccl")
     except RuntimeError as e:
         msgs.append(str(e))
+    try:  # the CU-sharing proxy (parallel/comm_proxy.py) models GPU collectives only
+        DataParallelEngine(store, comm_at_world1=True, comm="proxy")
+    except RuntimeError as e:
+        msgs.append(str(e))
     eng = DataParallelEngine(store, comm_at_world1=True, comm="c10d")
     msgs.append(eng.comm_plan()["comm_backend"])
     dist.destroy_process_group()
@@ -249,7 +253,7 @@ def test_comm_backend_selection_cpu(tmp_path, monkeypatch):
     p.join(timeout=60)
     assert p.exitcode == 0
     msgs = (tmp_path / "msgs.txt").read_text().splitlines()
-    assert "GPU" in msgs[0] and msgs[1] == "c10d"
+    assert "GPU" in msgs[0] and "GPU" in msgs[1] and msgs[2] == "c10d"
 
 
 def test_comm_exit_handler_does_not_pin_communicator():

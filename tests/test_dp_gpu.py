@@ -314,7 +314,7 @@ def _worker_proxy(port, out_dir):
     for _ in range(3):
         eng.train_step([(x.cuda(), y.cuda())])
         ref.train_step([(x.cuda(), y.cuda())])
-    proxy = eng.dp.proxy  # the engine may have rebuilt its buckets after step 1
+    assert eng.dp.proxy is proxy  # kept across the bucket relayout after step 1
     recs = proxy.take_records()
     assert recs and all(t > 0 for _, t in recs)
     a, b = eng.model_state_dict(), ref.model_state_dict()

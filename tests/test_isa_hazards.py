@@ -64,14 +64,14 @@ def test_attention_bwd64_asm_mfma_operands(tmp_path):
     text = out.read_text()
     m = re.search(r"^(_Z\S*attn_bwd64_kernel\S*):", text, re.M)
     body = text[m.end():text.find(".Lfunc_end", m.end())].split("\n")
-    hdrs = [i for i, l in enumerate(body) if "Loop Header: Depth=1" in l]
-    assert len(hdrs) == 2, "expected the diagonal-tile and steady-tile loops"
+    # the work-item loop (Depth=1) around the diagonal-tile and steady-tile loops (Depth=2)
+    hdrs = [i for i, l in enumerate(body) if "Loop Header: Depth=2" in l]
+    assert len(hdrs) == 2, "expected the diagonal-tile and steady-tile loops inside the item loop"
     labels = {l.split(":")[0].strip(): i for i, l in enumerate(body) if re.match(r"^\.LBB\w+:", l.strip())}
-    end = max(i for i, l in enumerate(body)
-              if (mm := re.search(r"s_c?branch\w*\s+(\.LBB\w+)", l)) and i > hdrs[1]
-              and labels.get(mm.group(1), 1 << 30) <= hdrs[1])
-    start = min(labels[mm.group(1)] for i, l in enumerate(body)
-                if (mm := re.search(r"s_c?branch\w*\s+(\.LBB\w+)", l)) and hdrs[1] < i <= end
-                and labels.get(mm.group(1), 1 << 30) <= hdrs[1])
+    # back edges of the steady loop: branches after its header to a label after the diagonal loop's
+    back = [(i, labels[mm.group(1)]) for i, l in enumerate(body)
+            if (mm := re.search(r"s_c?branch\w*\s+(\.LBB\w+)", l)) and i > hdrs[1]
+            and hdrs[0] < labels.get(mm.group(1), -1) <= hdrs[1]]
+    end, start = max(i for i, _ in back), min(t for _, t in back)
     scratch = [l.strip() for l in body[start:end + 1] if "scratch_" in l]
     assert not scratch, scratch[:5]
