@@ -5,7 +5,8 @@ without communication.
     python bench/comm_proxy.py --model gpt2 --batch 128 --configs 300:32:32,0:32:32,300:32:8
     python bench/comm_proxy.py --model gpt2-xl --batch 16 --configs 300:32:32
 
-Each config is ``gbps:channels:bucket_mb`` (gbps 0 = unpaced copy).  Per config, one JSON line:
+Each config is ``gbps:channels:bucket_mb[:ranks]`` (gbps 0 = unpaced copy; ranks 1 = a null
+proxy: the data-parallel engine's bucket plumbing with nothing launched).  Per config, one JSON line:
 step ms without communication (mean of the runs before and after), with the proxies, the
 slowdown, the step's exposed-communication time (end of backward to end of the last proxy), and
 per bucket its launch-to-completion time inside the step (from the moment its gradients were
@@ -82,10 +83,12 @@ def main():
     base_ms = [timed(base)[0]]
     print(f"# {a.model} B={a.batch}: no-comm step {base_ms[0]:.2f} ms", file=sys.stderr, flush=True)
     for spec in a.configs.split(","):
-        gbps, channels, bucket_mb = spec.split(":")
+        f = spec.split(":")
+        gbps, channels, bucket_mb = f[:3]
+        ranks = int(f[3]) if len(f) > 3 else a.ranks
         os.environ["MINGPT_PROXY_GBPS"] = gbps
         os.environ["MINGPT_PROXY_CHANNELS"] = channels
-        os.environ["MINGPT_PROXY_RANKS"] = str(a.ranks)
+        os.environ["MINGPT_PROXY_RANKS"] = str(ranks)
         eng = engine(True, float(bucket_mb))
         ms, recs, exposed = timed(eng, record=True)
         base_ms.append(timed(base)[0])
@@ -100,10 +103,10 @@ def main():
             nbytes = per[k][0][0]
             in_step = sum(t for _, t in per[k]) / len(per[k])
             rows.append({"bucket": k, "mib": round(nbytes / 2 ** 20, 2), "in_step_ms": round(in_step, 3),
-                         "isolated_ms": round(iso[k], 3), "ratio": round(in_step / iso[k], 2),
+                         "isolated_ms": round(iso[k], 3), "ratio": round(in_step / max(iso[k], 1e-6), 2),
                          "model_ms": None if proxy.model_ms(nbytes) is None else round(proxy.model_ms(nbytes), 3)})
         b0 = sum(base_ms[-2:]) / 2
-        out = {"model": a.model, "batch": a.batch, "ranks": a.ranks, "gbps": float(gbps), "channels": int(channels),
+        out = {"model": a.model, "batch": a.batch, "ranks": ranks, "gbps": float(gbps), "channels": int(channels),
                "bucket_mb": float(bucket_mb), "n_buckets": nb, "step_ms_no_comm": round(b0, 2),
                "step_ms_proxy": round(ms, 2), "slowdown_pct": round((ms / b0 - 1) * 100, 2),
                "exposed_comm_ms": None if exposed is None else round(exposed, 3),

@@ -71,12 +71,56 @@ def use_for(tokens: int) -> bool:
     return _ENABLED and (_MODE != "auto" or tokens <= _AUTO_TOKENS)
 
 
+# HIP stream priority of the side stream (MINGPT_WGRAD_PRIORITY; lower = higher priority, 0 the
+# default) and of the compute stream the engine runs forward + backward on
+# (MINGPT_COMPUTE_PRIORITY): "auto" (default) = high (-1) whenever the side stream is in use for
+# the batch, "off" = the caller's current stream, an integer = always that priority.  The
+# dispatcher prefers the higher-priority queue's workgroups when a CU frees, so the critical
+# path's kernels (LayerNorm backward, data gradients) stop waiting behind side-stream weight-
+# gradient tiles: gpt2-xl B = 16 +3.3 %, 92.5k / 91.7k vs 89.2k / 89.1k tok/s on one box
+# (profiles/round6_compute_priority_ab.txt); no change where the side stream is off
+_SIDE_PRIO = int(os.environ.get("MINGPT_WGRAD_PRIORITY", "0"))
+_COMPUTE_PRIO = os.environ.get("MINGPT_COMPUTE_PRIORITY", "auto").lower()
+_compute: Dict[Tuple[int, int], "torch.cuda.Stream"] = {}
+
+
 def _stream(dev: torch.device) -> "torch.cuda.Stream":
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     s = _side.get(idx)
     if s is None:
-        s = _side[idx] = torch.cuda.Stream(device=idx)
+        s = _side[idx] = torch.cuda.Stream(device=idx, priority=_SIDE_PRIO)
     return s
+
+
+def compute_priority(tokens: int):
+    """The compute stream's priority for a batch of ``tokens`` rows (None: the current stream)."""
+    if _COMPUTE_PRIO in ("off", "none", ""):
+        return None
+    if _COMPUTE_PRIO == "auto":
+        return -1 if use_for(tokens) else None
+    return int(_COMPUTE_PRIO)
+
+
+@contextlib.contextmanager
+def compute_stream(device: torch.device, tokens: int):
+    """Run the enclosed forward + backward on a stream of priority :func:`compute_priority`
+    (ordered after, and joined back into, the caller's current stream); a no-op on CPU or when
+    no priority applies."""
+    prio = compute_priority(tokens) if device.type == "cuda" else None
+    if prio is None:
+        yield
+        return
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _compute.get((idx, prio))
+    if s is None:
+        s = _compute[(idx, prio)] = torch.cuda.Stream(device=idx, priority=prio)
+    cur = torch.cuda.current_stream(idx)
+    s.wait_stream(cur)
+    try:
+        with torch.cuda.stream(s):
+            yield
+    finally:
+        cur.wait_stream(s)
 
 
 def run_wgrad(fn: Callable[[], None], *inputs: torch.Tensor) -> None:

@@ -15,7 +15,8 @@ bucket-ready point on the same stream hand-off as the real collective; gradients
 they are (the proxy writes a scratch buffer), so the step's arithmetic is the one-GPU step's.
 ``bench/comm_proxy.py`` reports each proxy's launch-to-completion time inside the step (from the
 moment its bucket was ready on the device) against its isolated time, and the step slowdown.
-Environment: ``MINGPT_PROXY_RANKS`` (N, default 8), ``MINGPT_PROXY_CHANNELS`` (workgroups,
+Environment: ``MINGPT_PROXY_RANKS`` (N, default 8; 1 = a null proxy that launches nothing, to
+separate the data-parallel plumbing from the CU sharing), ``MINGPT_PROXY_CHANNELS`` (workgroups,
 default 32), ``MINGPT_PROXY_GBPS`` (bus bandwidth, default 300; 0 = unpaced).
 """
 from __future__ import annotations
@@ -50,8 +51,9 @@ class CommProxy:
         self.ranks = int(ranks if ranks is not None else env("MINGPT_PROXY_RANKS", "8"))
         self.channels = int(channels if channels is not None else env("MINGPT_PROXY_CHANNELS", "32"))
         self.gbps = float(gbps if gbps is not None else env("MINGPT_PROXY_GBPS", "300"))
-        if self.ranks < 2 or not 0 < self.channels <= 1024 or self.gbps < 0:
-            raise ValueError(f"comm proxy: ranks {self.ranks} (>= 2), channels {self.channels}, gbps {self.gbps}")
+        # ranks 1: a null proxy (nothing moved, no kernel): the data-parallel plumbing alone
+        if self.ranks < 1 or not 0 < self.channels <= 1024 or self.gbps < 0:
+            raise ValueError(f"comm proxy: ranks {self.ranks} (>= 1), channels {self.channels}, gbps {self.gbps}")
         self.device = device
         self.stream = torch.cuda.Stream(device=device)  # RCCL runs on a stream of its own
         self._scratch: Optional[torch.Tensor] = None

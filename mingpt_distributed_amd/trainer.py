@@ -179,7 +179,7 @@ class StepEngine:
 
     def forward_backward(self, x, y, scale: float = 1.0, sync: bool = True):
         ctx = self.dp.no_sync() if (self.dp is not None and not sync) else contextlib.nullcontext()
-        with ctx:
+        with ctx, streams.compute_stream(self.device, x.numel()):
             with self._range("mingpt::forward"):
                 _, loss = self.model(x, y)
             with self._range("mingpt::backward"):

@@ -295,7 +295,8 @@ def _worker_proxy(port, out_dir):
     runs on its own stream at the bucket-ready point, leaves the gradients alone (the weights
     match a no-communication engine's), is waited on before the optimizer, and lasts its paced
     time when alone on the GPU."""
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MINGPT_PROXY_GBPS="50",
+    # 1 GB/s: the 0.5 MiB buckets of this small model last ~1 ms each, well above launch overhead
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MINGPT_PROXY_GBPS="1",
                       MINGPT_PROXY_CHANNELS="16", MINGPT_PROXY_RANKS="8")
     import torch.distributed as dist
 
@@ -323,7 +324,8 @@ def _worker_proxy(port, out_dir):
     iso = eng.dp.time_collectives(reps=3)
     for bk, t in zip(eng.dp.buckets, iso):
         m = proxy.model_ms((bk.end - bk.start) * 4)
-        assert 0.8 * m < t < 1.5 * m + 0.05, (t, m)
+        if m >= 0.2:  # (tiny buckets: launch and event overhead)
+            assert 0.8 * m < t < 1.3 * m + 0.1, (t, m)
     dist.destroy_process_group()
 
 

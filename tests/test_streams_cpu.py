@@ -63,3 +63,22 @@ def test_ddp_launch_uses_collective_context(monkeypatch):
     b = _B()
     e._launch(b)
     assert entered == [torch.device("cpu")] and b.work == "work"
+
+
+def test_compute_priority_modes(monkeypatch):
+    """MINGPT_COMPUTE_PRIORITY: "auto" raises the compute stream's priority exactly where the
+    side stream runs the weight gradients; "off" never; an integer always; CPU: no stream."""
+    prev = (streams._ENABLED, streams._MODE)
+    try:
+        streams.set_enabled(True, "auto")
+        monkeypatch.setattr(streams, "_COMPUTE_PRIO", "auto")
+        assert streams.compute_priority(16384) == -1
+        assert streams.compute_priority(131072) is None
+        monkeypatch.setattr(streams, "_COMPUTE_PRIO", "off")
+        assert streams.compute_priority(16384) is None
+        monkeypatch.setattr(streams, "_COMPUTE_PRIO", "-1")
+        assert streams.compute_priority(131072) == -1
+        with streams.compute_stream(torch.device("cpu"), 16):
+            pass  # a no-op on the CPU
+    finally:
+        streams._ENABLED, streams._MODE = prev
