@@ -28,16 +28,23 @@ h, wl = r(M, D), r(V, D)
 shapes.append(("lmhead_fwd", M, V, D, lambda: torch.mm(h, wl.t()), lambda: G.gemm_nt(h, wl, ld=V)))
 dl, wlt = r(M, V), wl.t().contiguous()
 shapes.append(("lmhead_dgrad", M, D, V, lambda: torch.mm(dl, wl), lambda: G.gemm_nt(dl, wlt)))
+ROUNDS = int(os.environ.get("ROUNDS", "3"))
 for nm, m, n, k, blas, ours in shapes:
     fl = 2.0 * m * n * k
-    t = timeit(blas)
-    out = {"hipblaslt": [round(t * 1e3, 1), round(fl / t / 1e9)]}
-    for v in (0, 1, 5, 6):
-        C.gemm_set_variant(v)
-        try:
-            t = timeit(ours)
-            out[names[v]] = [round(t * 1e3, 1), round(fl / t / 1e9)]
-        except Exception as e:
-            out[names[v]] = str(e)[:50]
+    # every candidate ROUNDS times, interleaved (the clock drifts with the load: a fixed order
+    # favoured whatever ran first or last); each entry is the best round's median
+    best = {}
+    for _ in range(ROUNDS):
+        t = timeit(blas)
+        best["hipblaslt"] = min(best.get("hipblaslt", 1e9), t)
+        for v in (0, 1, 5, 6):
+            C.gemm_set_variant(v)
+            try:
+                t = timeit(ours)
+                prev = best.get(names[v], 1e9)
+                best[names[v]] = t if isinstance(prev, str) else min(prev, t)
+            except Exception as e:
+                best[names[v]] = str(e)[:50]
     C.gemm_set_variant(0)
+    out = {k_: (v_ if isinstance(v_, str) else [round(v_ * 1e3, 1), round(fl / v_ / 1e9)]) for k_, v_ in best.items()}
     print(json.dumps({"shape": nm, "M": m, "N": n, "K": k, "us_tflops": out}), flush=True)
