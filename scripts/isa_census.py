@@ -13,7 +13,7 @@ are by mnemonic (a census, not a dataflow analysis):
 
   mfma          v_mfma_*
   exp           v_exp_f32 (softmax recompute)
-  softmax-math  float mul / fma / add / sub, packed f32, v_bfe_i32 / v_and (dropout keep select)
+  softmax-math  float mul / fma / add / sub / max (max3), packed f32, v_bfe_i32 / v_and (dropout keep select)
   bf16-pack     v_cvt_pk_bf16_f32, v_perm_b32
   address       integer add / shift / xor / or / bitop3 / mad on addresses and indices
   compare-sel   v_cmp*, v_cndmask* (causal mask, bounds)
@@ -28,7 +28,7 @@ CATS = [
     ("mfma", r"^v_mfma"),
     ("exp", r"^v_exp_f32"),
     ("bf16-pack", r"^v_cvt_pk_bf16|^v_perm_b32"),
-    ("softmax-math", r"^v_(pk_)?(mul|fma|add|sub|max|min)_f32|^v_bfe_i32|^v_and_b32"),
+    ("softmax-math", r"^v_(pk_)?(mul|fma|add|sub|max|min)_f32|^v_(max3|min3|med3)_f32|^v_bfe_i32|^v_and_b32"),
     ("compare-sel", r"^v_cmp|^v_cndmask"),
     ("move", r"^v_mov|^v_readfirstlane|^v_accvgpr|^v_readlane|^v_writelane"),
     ("address", r"^v_(add|sub|lshl|lshr|ashr|xor|or|and|bitop3|mad|mul_lo|mul_u32|bfe_u32|bfi|add3|lshl_add|lshl_or|add_lshl|and_or|or3|min|max)"),
