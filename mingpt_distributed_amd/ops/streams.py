@@ -107,7 +107,9 @@ def compute_stream(device: torch.device, tokens: int):
     (ordered after, and joined back into, the caller's current stream); a no-op on CPU or when
     no priority applies."""
     prio = compute_priority(tokens) if device.type == "cuda" else None
-    if prio is None:
+    # not inside a hipGraph capture: a fork onto a stream of another priority there crashed
+    # capture_end (segfault in tests/test_dropout_grad_gpu.py's graph test); replays run without it
+    if prio is None or torch.cuda.is_current_stream_capturing():
         yield
         return
     idx = device.index if device.index is not None else torch.cuda.current_device()
