@@ -26,8 +26,7 @@ __global__ __launch_bounds__(256) void comm_proxy_kernel(const uint4* __restrict
   const long i0 = (long)blockIdx.x * per;
   const long i1 = i0 + per < total16 ? i0 + per : total16;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  long chunk = 0;
-  for (long c = i0; c < i1; c += 256 * kChunk, ++chunk) {
+  for (long c = i0; c < i1; c += 256 * kChunk) {
     uint4 v[kChunk];
 #pragma unroll
     for (int k = 0; k < kChunk; ++k) {
@@ -41,8 +40,9 @@ __global__ __launch_bounds__(256) void comm_proxy_kernel(const uint4* __restrict
       if (i >= n16) i -= n16;
       if (c + k * 256 + threadIdx.x < i1) dst[i] = v[k];
     }
-    if (ticks_per_chunk > 0) {  // hold the CU until this chunk's share of the link time is spent
-      const unsigned long long due = t0 + (unsigned long long)(chunk + 1) * ticks_per_chunk;
+    if (ticks_per_chunk > 0) {  // hold the CU until the link time of the units moved so far is spent
+      const long done = (c + 256 * kChunk < i1 ? c + 256 * kChunk : i1) - i0;  // a partial last chunk: its share
+      const unsigned long long due = t0 + (((unsigned long long)done * ticks_per_chunk) >> 10);
       while (__builtin_amdgcn_s_memrealtime() < due) __builtin_amdgcn_s_sleep(4);
     }
   }
