@@ -35,7 +35,7 @@ from __future__ import annotations
 import contextlib
 import os
 from collections import deque
-from typing import Callable, Deque, Dict, Tuple
+from typing import Callable, Deque, Dict, Optional, Tuple
 
 import torch
 
@@ -46,6 +46,11 @@ import torch
 _MODE = os.environ.get("MINGPT_WGRAD_STREAM", "auto").lower()
 _ENABLED = _MODE != "0"
 _AUTO_TOKENS = int(os.environ.get("MINGPT_WGRAD_STREAM_TOKENS", "16384"))
+# ... and for models at least this wide (the weight gradients' smaller dimension): below it the
+# GEMMs are launch-bound and the stream hand-offs cost more than the overlap gives (gpt-mini,
+# D = 192: hipGraph step 4.73M tok/s single-stream vs 4.39M with the side stream,
+# profiles/round6_compute_priority_ab.txt)
+_AUTO_WIDTH = int(os.environ.get("MINGPT_WGRAD_STREAM_WIDTH", "512"))
 # weight gradients in flight before the compute stream waits for the oldest (4 = one block)
 _LAG = max(1, int(os.environ.get("MINGPT_WGRAD_LAG", "4")))
 _side: Dict[int, "torch.cuda.Stream"] = {}
@@ -66,9 +71,9 @@ def set_enabled(on: bool, mode: str = "1") -> None:
     _MODE = mode if on else "0"
 
 
-def use_for(tokens: int) -> bool:
+def use_for(tokens: int, width: Optional[int] = None) -> bool:
     """Whether a weight gradient over ``tokens`` rows goes to the side stream."""
-    return _ENABLED and (_MODE != "auto" or tokens <= _AUTO_TOKENS)
+    return _ENABLED and (_MODE != "auto" or (tokens <= _AUTO_TOKENS and (width is None or width >= _AUTO_WIDTH)))
 
 
 # HIP stream priority of the side stream (MINGPT_WGRAD_PRIORITY; lower = higher priority, 0 the
@@ -92,21 +97,22 @@ def _stream(dev: torch.device) -> "torch.cuda.Stream":
     return s
 
 
-def compute_priority(tokens: int):
-    """The compute stream's priority for a batch of ``tokens`` rows (None: the current stream)."""
+def compute_priority(tokens: int, width: Optional[int] = None):
+    """The compute stream's priority for a batch of ``tokens`` rows of a model ``width`` wide
+    (None: the current stream)."""
     if _COMPUTE_PRIO in ("off", "none", ""):
         return None
     if _COMPUTE_PRIO == "auto":
-        return -1 if use_for(tokens) else None
+        return -1 if use_for(tokens, width) else None
     return int(_COMPUTE_PRIO)
 
 
 @contextlib.contextmanager
-def compute_stream(device: torch.device, tokens: int):
+def compute_stream(device: torch.device, tokens: int, width: Optional[int] = None):
     """Run the enclosed forward + backward on a stream of priority :func:`compute_priority`
     (ordered after, and joined back into, the caller's current stream); a no-op on CPU or when
     no priority applies."""
-    prio = compute_priority(tokens) if device.type == "cuda" else None
+    prio = compute_priority(tokens, width) if device.type == "cuda" else None
     # not inside a hipGraph capture: a fork onto a stream of another priority there crashed
     # capture_end (segfault in tests/test_dropout_grad_gpu.py's graph test); replays run without it
     if prio is None or torch.cuda.is_current_stream_capturing():
@@ -127,7 +133,7 @@ def compute_stream(device: torch.device, tokens: int):
 
 def run_wgrad(fn: Callable[[], None], *inputs: torch.Tensor) -> None:
     """Run ``fn`` (a weight-gradient accumulation reading ``inputs``) on the side stream."""
-    if not inputs[0].is_cuda or not use_for(inputs[0].shape[0]):
+    if not inputs[0].is_cuda or not use_for(inputs[0].shape[0], min(t.shape[-1] for t in inputs)):
         fn()
         return
     dev = inputs[0].device

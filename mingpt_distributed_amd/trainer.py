@@ -179,7 +179,8 @@ class StepEngine:
 
     def forward_backward(self, x, y, scale: float = 1.0, sync: bool = True):
         ctx = self.dp.no_sync() if (self.dp is not None and not sync) else contextlib.nullcontext()
-        with ctx, streams.compute_stream(self.device, x.numel()):
+        width = getattr(getattr(self.model, "config", None), "n_embd", None)
+        with ctx, streams.compute_stream(self.device, x.numel(), width):
             with self._range("mingpt::forward"):
                 _, loss = self.model(x, y)
             with self._range("mingpt::backward"):

@@ -73,6 +73,9 @@ def test_compute_priority_modes(monkeypatch):
         streams.set_enabled(True, "auto")
         monkeypatch.setattr(streams, "_COMPUTE_PRIO", "auto")
         assert streams.compute_priority(16384) == -1
+        assert streams.compute_priority(16384, 1600) == -1  # gpt2-xl at B = 16
+        assert streams.compute_priority(8192, 192) is None  # gpt-mini: launch-bound, no side stream
+        assert not streams.use_for(8192, 192) and streams.use_for(8192, 768)
         assert streams.compute_priority(131072) is None
         monkeypatch.setattr(streams, "_COMPUTE_PRIO", "off")
         assert streams.compute_priority(16384) is None
