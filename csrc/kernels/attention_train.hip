@@ -759,9 +759,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
     const uint32_t lb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(smem + OFF_DS);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int pc = 8 * wv + i;  // rows 8 pc ..
-      dma_dwordx4(rk_, v0, (uint32_t)(8 * pc * ld * 2), lb + pc * 1024);
-      dma_dwordx4(rv_, v0, (uint32_t)(8 * pc * ld * 2), lb + KB * ROWB + pc * 1024);
+      const int pc = 8 * wv + i;  // rows 8 pc ..: in voffset, the part the range check sees
+      const uint32_t v = v0 + (uint32_t)(8 * pc * ld * 2);
+      dma_dwordx4(rk_, v, 0, lb + pc * 1024);
+      dma_dwordx4(rv_, v, 0, lb + KB * ROWB + pc * 1024);
     }
   };
   bf16x8 vf[2][NKS];  // this wave's V rows (dP~'s B operand), group g = keys 64 w + 32 g + lane
@@ -836,44 +837,50 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
   // Without dropout the LDS words are set to all-ones once.  Row constants: waves 0-1 load lse,
   // waves 2-3 delta (threads [0, BQ) / [BQ, 2 BQ)); rows past T read 0 (descriptor extent) and
   // are replaced at commit.
-  auto issue = [&](int ib, int ihh, int ibh, int ikb0, int qt, int par) {
-    const int it0w = (ikb0 / 64) * 2;
+  // descriptors of the item whose tiles issue() stages, built once per item (set_issue_item), not
+  // per tile: the 64-bit origin arithmetic of four descriptors ran on the CU's one scalar unit for
+  // all four waves at every tile.  Every row-dependent offset rides in voffset -- the part the
+  // hardware range-checks -- so rows past the end of a tensor read 0.
+  u32x4_t dmw = {0u, 0u, 0u, 0u}, ddo;
+  __amdgpu_buffer_rsrc_t dqr, dlr;
+  int dt0w = 0;
+  auto set_issue_item = [&](int ib, int ihh, int ibh, int ikb0) {
+    dt0w = (ikb0 / 64) * 2;
+    if (a.thr) dmw = kv_rsrc_words(a.dmask, (uint64_t)(ibh + 1) * ntw * a.T * 4, (uint64_t)ibh * ntw * a.T * 4);
+    ddo = kv_rsrc_words(a.dout, do_total, ((uint64_t)ib * a.T * a.D + (uint64_t)ihh * 64) * 2);
+    dqr = kv_rsrc(a.qkv, q_total, ((uint64_t)ib * a.T * ld + (uint64_t)ihh * 64) * 2);
+    dlr = kv_rsrc(reinterpret_cast<const bf16_t*>((w >= 2 ? a.delta : a.lse) + (long)ibh * a.T), (uint64_t)a.T * 4, 0);
+  };
+  auto issue = [&](int qt, int par) {
     int t = threadIdx.x;
     asm volatile("" : "+v"(t));
     if (a.thr) {  // keep words straight into LDS buffer par, issued first (see commit)
-      const u32x4_t mw_rs = kv_rsrc_words(a.dmask, (uint64_t)(ibh + 1) * ntw * a.T * 4, (uint64_t)ibh * ntw * a.T * 4);
-      const uint32_t vmw = (uint32_t)(((t >> 7) * a.T + (t & (BQ - 1))) * 4);
+      const uint32_t vmw = (uint32_t)(((t >> 7) * a.T + (t & (BQ - 1)) + dt0w * a.T + qt * BQ) * 4);
       const uint32_t lb = __builtin_amdgcn_readfirstlane(
           (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(smem + OFF_MW + par * MWB + 64 * 4 * (threadIdx.x >> 6)));
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        dma_dword(mw_rs, vmw, (uint32_t)(((it0w + 2 * i) * a.T + qt * BQ) * 4), lb + NT * 4 * i);
+      for (int i = 0; i < 4; ++i) dma_dword(dmw, vmw + (uint32_t)(2 * i * a.T * 4), 0, lb + NT * 4 * i);
     }
     {  // dO straight into its LDS image for tile qt (buffer par): 16 pieces of 8 rows x 128 B,
        // 4 per wave; lane -> (row 8 p + lane / 8, stored chunk lane % 8), the swizzle applied on
        // the source side (logical chunk = stored ^ swz(row); swz's bit 2 follows the piece parity)
-      const uint64_t do_org = ((uint64_t)ib * a.T * a.D + (uint64_t)ihh * 64) * 2;
-      const u32x4_t rsd = kv_rsrc_words(a.dout, do_total, do_org + (uint64_t)qt * BQ * a.D * 2);
       const int ln = t & 63, r8 = ln >> 3;
-      const uint32_t v0 = (uint32_t)(r8 * a.D * 2 + (((ln & 7) ^ swz(r8)) << 4));
-      const uint32_t v1 = (uint32_t)(r8 * a.D * 2 + (((ln & 7) ^ swz(r8 + 8)) << 4));
+      const uint32_t vt = (uint32_t)((qt * BQ + r8) * a.D * 2);
+      const uint32_t v0 = vt + (uint32_t)((((ln & 7) ^ swz(r8)) << 4));
+      const uint32_t v1 = vt + (uint32_t)((((ln & 7) ^ swz(r8 + 8)) << 4));
       const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
       const uint32_t lb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(smem + (par ? OFF_DO2 : OFF_DO));
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int pc = 4 * wv + i;  // piece: rows 8 pc ..
-        dma_dwordx4(rsd, (i & 1) ? v1 : v0, (uint32_t)(8 * pc * a.D * 2), lb + pc * 1024);
+        dma_dwordx4(ddo, ((i & 1) ? v1 : v0) + (uint32_t)(8 * pc * a.D * 2), 0, lb + pc * 1024);
       }
     }
-    const uint64_t q_org = ((uint64_t)ib * a.T * ld + (uint64_t)ihh * 64) * 2;
-    const uint32_t vq = (uint32_t)((t >> 3) * ld * 2 + (t & 7) * 16);
-    const __amdgpu_buffer_rsrc_t rsq = kv_rsrc(a.qkv, q_total, q_org + (uint64_t)qt * BQ * ld * 2);
+    const uint32_t vq = (uint32_t)(((t >> 3) + qt * BQ) * ld * 2 + (t & 7) * 16);
 #pragma unroll
     for (int c = 0; c < 4; ++c)
-      rq[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsq, vq, (int)(c * 32 * ld * 2), 0));
-    const __amdgpu_buffer_rsrc_t rs_l = kv_rsrc(reinterpret_cast<const bf16_t*>((w >= 2 ? a.delta : a.lse) + (long)ibh * a.T),
-                                                (uint64_t)a.T * 4, 0);
-    rl_raw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_l, (t & (BQ - 1)) * 4, qt * BQ * 4, 0));
+      rq[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(dqr, vq + (uint32_t)(c * 32 * ld * 2), 0, 0));
+    rl_raw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dlr, (uint32_t)(((t & (BQ - 1)) + qt * BQ) * 4), 0, 0));
   };
   auto commit = [&](int qt) {
     // this wave's DMA'd dO rows and keep words (issued before every load waited for here) have
@@ -896,7 +903,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
     for (int i = 0; i < 8; ++i) reinterpret_cast<uint32_t*>(smem + OFF_MW)[threadIdx.x + NT * i] = 0xffffffffu;
   }
   int par = 0;  // LDS buffer parity of the current tile's dO image and keep words
-  issue(b, hh, bh, kb0, qt0, par);
+  set_issue_item(b, hh, bh, kb0);
+  issue(qt0, par);
   if (threadIdx.x == 0) *sItem = atomicAdd(a.work, 1) + (int)gridDim.x;  // the item after this one
   commit(qt0);  // its vmcnt(0) covers dma_kv
   __syncthreads();
@@ -917,7 +925,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
     const char* const sdO = smem + (par ? OFF_DO2 : OFF_DO);  // this tile's dO image
     BWD64_STAMP(qt - qt0, 0);
     const int qn = more ? qt + 1 : nkb0 / BQ;  // the next tile: this item's, or the next item's first
-    if (more || has_next) issue(more ? b : nb, more ? hh : nhh, more ? bh : nbh, more ? kb0 : nkb0, qn, par ^ 1);
+    if (!more && has_next) set_issue_item(nb, nhh, nbh, nkb0);
+    if (more || has_next) issue(qn, par ^ 1);
     BWD64_STAMP(qt - qt0, 1);
     // one 128-query tile: 8 units (subtile qs = u / 2, key group g = u % 2) in a three-deep
     // software pipeline.  Stage u (0..8) is 16 slots, each ONE MFMA plus one element of unit u's
