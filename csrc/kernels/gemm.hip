@@ -1213,9 +1213,9 @@ int pick_config(int M, int N, int K, int layout) {
   const long t256 = tm * cdiv(N, 256);
   if (layout == 0) {
     if (t256 < 256) return 1;
-    // long-K, narrow outputs (the LM head's data gradient: N = 768, K = 50304): the 128x96 wave
-    // tile measured 3.75 vs 4.19 ms (bench/gemm_blas_shapes.py); at short K the 256-wide tile wins
-    if (K >= 8192 && N % 192 == 0 && N <= 1536) return 6;
+    // (the LM head's data gradient, N = 768, K = 50304, went to the 128x96 wave tile until round 6:
+    // with interleaved timing the 256-wide tile is 2.1-2.4 % faster at 65k and 131k tokens,
+    // profiles/round6_gemm_vs_hipblaslt_*.jsonl)
     // W4 width: fewer (rounds x tile width) on the 256 CUs wins; the 96-wide wave tile costs ~8 %
     // more per FLOP (more LDS reads per MFMA), so it must save more than that
     const long r256 = (t256 + 255) / 256 * 256, r192 = (tm * cdiv(N, 192) + 255) / 256 * 192;
