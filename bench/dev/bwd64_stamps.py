@@ -21,7 +21,8 @@ for _ in range(4):
 torch.cuda.synchronize()
 raw = C.attention_bwd64_stamps()
 st = raw[:64 * 4 * 8 * 8].view(64, 4, 8, 8).double()
-pe = raw[64 * 4 * 8 * 8:].view(64, 4, 4, 2).double()
+pe2 = raw[64 * 4 * 8 * 8:].view(64, 4, 2, 4, 2).double()  # [wg][wave][item 0 / 1][point][memtime, realtime]
+pe = pe2[:, :, 0]
 names = ["issue", "tile body", "barrier 1", "commit", "dQ MFMA", "dQ store", "barrier 2"]
 print("phase cycles (median over workgroups and waves), tiles 0-1 diagonal, 2-7 steady")
 print(f"{'tile':>4s} " + " ".join(f"{n:>10s}" for n in names) + f" {'total':>8s}")
@@ -39,3 +40,10 @@ clk = ((pe[:, :, 3, 0] - pe[:, :, 0, 0]) / (pe[:, :, 3, 1] - pe[:, :, 0, 1]) * 0
 wall = ((pe[:, :, 3, 1] - pe[:, :, 0, 1]) / 100).median().item()
 print(f"workgroup (key block 0): prologue {pro:.0f}, tile loops {loop:.0f}, epilogue {epi:.0f} cycles; "
       f"{wall:.1f} us at {clk:.2f} GHz")
+# the second work item (the workgroup's next item from the counter: its prologue is the K / V
+# conversion after the first item's epilogue; its first tile and K / V were staged under it)
+q = pe2[:, :, 1]
+pro2 = (q[:, :, 1, 0] - q[:, :, 0, 0]).median().item()
+loop2 = (q[:, :, 2, 0] - q[:, :, 1, 0]).median().item()
+epi2 = (q[:, :, 3, 0] - q[:, :, 2, 0]).median().item()
+print(f"second item: prologue {pro2:.0f}, tile loops {loop2:.0f}, epilogue {epi2:.0f} cycles")

@@ -719,7 +719,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attention_set_bwd64", &mg::attention_set_bwd64);
 #ifdef MG_BWD64_STAMPS
   m.def("attention_bwd64_stamps", []() {
-    auto t = at::empty({64 * 4 * 8 * 8 + 64 * 4 * 8}, at::kLong);
+    auto t = at::empty({64 * 4 * 8 * 8 + 64 * 4 * 16}, at::kLong);
     mg::attention_bwd64_stamps(reinterpret_cast<unsigned long long*>(t.data_ptr<int64_t>()));
     return t;
   });

@@ -620,19 +620,19 @@ MG_DEVICE void keep_live(const f32x16& v) { asm volatile("" ::"v"(v)); }
 // Diagnostic build only (-DMG_BWD64_STAMPS): s_memtime per wave at 8 points of each tile of the
 // first 64 workgroups (bench/dev/bwd64_stamps.py reads them back).  Nothing else reads this buffer.
 __device__ unsigned long long g_bwd64_stamps[64 * 4 * 8 * 8];
-// per wave: s_memtime and s_memrealtime (100 MHz) at kernel start, before the tile loops, after
-// them, and at the end
-__device__ unsigned long long g_bwd64_pe[64 * 4 * 8];
+// per wave and for its first two work items: s_memtime and s_memrealtime (100 MHz) at the item's
+// start (kernel start / the previous item's end), before the tile loops, after them, and at its end
+__device__ unsigned long long g_bwd64_pe[64 * 4 * 16];
 #define BWD64_PE(pt)                                                                               \
   do {                                                                                             \
-    if (bwd64_first && blockIdx.x < 64 && (threadIdx.x & 63) == 0) {                               \
-      g_bwd64_pe[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + 2 * (pt)] = __builtin_amdgcn_s_memtime(); \
-      g_bwd64_pe[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + 2 * (pt) + 1] = __builtin_amdgcn_s_memrealtime(); \
+    if (bwd64_it < 2 && blockIdx.x < 64 && (threadIdx.x & 63) == 0) {                              \
+      g_bwd64_pe[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + 8 * bwd64_it + 2 * (pt)] = __builtin_amdgcn_s_memtime(); \
+      g_bwd64_pe[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + 8 * bwd64_it + 2 * (pt) + 1] = __builtin_amdgcn_s_memrealtime(); \
     }                                                                                              \
   } while (0)
 #define BWD64_STAMP(tile, pt)                                                                      \
   do {                                                                                             \
-    if (bwd64_first && blockIdx.x < 64 && (tile) < 8 && (threadIdx.x & 63) == 0)                   \
+    if (bwd64_it == 0 && blockIdx.x < 64 && (tile) < 8 && (threadIdx.x & 63) == 0)                 \
       g_bwd64_stamps[((blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (tile)) * 8 + (pt)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
@@ -701,7 +701,7 @@ MG_DEVICE void dma_dword(const u32x4_t& rs, uint32_t voff, uint32_t soff, uint32
 // Register budget: dK^T / dV^T of 2 groups (128), K / V fragments (64), two S / dP~ pairs (64), the
 // next tile's staged Q / dO (32), row constants of two subtiles (64), operand fragments.
 __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
-  [[maybe_unused]] bool bwd64_first = true;  // stamps (diagnostic build): the first item only
+  [[maybe_unused]] int bwd64_it = 0;  // stamps (diagnostic build): the work item's ordinal
   BWD64_PE(0);
   constexpr int BQ = 128, KB = 256, NT = 256, NKS = 4, NO = 2, KW = 8;
   constexpr int HQ = BQ * ROWB;
@@ -1215,6 +1215,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
   if (threadIdx.x == 0 && has_next) *sItem = atomicAdd(a.work, 1) + (int)gridDim.x;
   BWD64_PE(3);
   if (!has_next) break;
+  ++bwd64_it;
+  BWD64_PE(0);  // the next item's start (stamps): its prologue follows
   // ---- the next item's prologue: its first tile was staged by the last tile, its K / V rows
   // DMA'd under the epilogue
   item = nxt;
@@ -1224,7 +1226,6 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
   __syncthreads();
   convert_kv();
   __syncthreads();
-  bwd64_first = false;
   }
 }
 
