@@ -769,10 +769,14 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
   // after dma_kv landed (vmcnt(0) + barrier): K <- c K into its LDS image (dQ's B operand; the K
   // fragments of the chains come from it), this wave's V fragments into registers
   auto convert_kv = [&]() {
+    // addresses from an opaque thread id: hoisted out of the item loop they were spilled, and the
+    // reload's vmcnt(0) made the item transition wait for the epilogue's stores after all
+    int tt = threadIdx.x;
+    asm volatile("" : "+v"(tt));
     uint4 rk[stk::N];
 #pragma unroll
     for (int i = 0; i < stk::N; ++i) {
-      const int idx = threadIdx.x + NT * i, rem = idx % (KB * 8);
+      const int idx = tt + NT * i, rem = idx % (KB * 8);
       rk[i] = *reinterpret_cast<const uint4*>(sdS + (rem >> 3) * ROWB + (rem & 7) * 16);
       float f[8];
       unpack8(rk[i], f);
@@ -780,12 +784,17 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
       for (int j = 0; j < 8; ++j) f[j] *= a.scale_log2;
       rk[i] = pack8(f);
     }
-    stk::store(sK, rk);
+#pragma unroll
+    for (int c = 0; c < stk::N; ++c) {  // stk::store with the opaque thread id
+      const int idx = tt + NT * c, rem = idx % (KB * 8);
+      *reinterpret_cast<uint4*>(sK + (idx / (KB * 8)) * KB * ROWB + lds_off(rem >> 3, rem & 7)) = rk[c];
+    }
 #pragma unroll
     for (int g = 0; g < 2; ++g)
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks)
-        vf[g][ks] = *reinterpret_cast<const bf16x8*>(sdS + KB * ROWB + (64 * w + 32 * g + l32) * ROWB + ks * 32 + 16 * h32);
+        vf[g][ks] = *reinterpret_cast<const bf16x8*>(sdS + KB * ROWB + ((tt >> 6) * 64 + 32 * g + (tt & 31)) * ROWB +
+                                                     ks * 32 + 16 * ((tt >> 5) & 1));
   };
   dma_kv(b, hh, kb0);
   // dropout: both groups read the same keep word of a row (the 64-key tile of keys 64 w..), the
@@ -912,6 +921,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
   __syncthreads();
 
   int nxt = 0, nbh = 0, nb = 0, nhh = 0, nkb0 = 0;  // the next item (valid if has_next)
+  int nn_raw = 0;  // thread 0: the counter value of the item after the next one
   bool has_next = false;
   // one 128-query tile; DIAG: some key of the block follows some query of the tile.  The diagonal
   // tiles (the first two of the block) and the rest run in two loops, each with ONE instance of the
@@ -1072,6 +1082,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
     __syncthreads();  // dS^T of all 256 keys in LDS
     BWD64_STAMP(qt - qt0, 3);
     if (more || has_next) commit(qn);  // the dQ products read only dS^T and K
+    // the item after the next one, fetched here (after commit's vmcnt(0)), so that its return is
+    // long in by the epilogue's end, where it is published: a wait for it there would also wait
+    // for every store issued before it
+    if (!more && has_next && threadIdx.x == 0) nn_raw = atomicAdd(a.work, 1);
     BWD64_STAMP(qt - qt0, 4);
     // dQ[32 queries of subtile w][64] = dS (c K), over the keys that precede some query of it
     const int q0w = qbase + 32 * w;
@@ -1140,7 +1154,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
   // row; one v_permlane32_swap per dword gives each the 8 contiguous columns of a 16-column step
   // (lanes < 32: columns 16 k .. + 7, the others 16 k + 8 .. + 15): half the store instructions
   // of the row-per-lane 8-byte form, which was store-issue bound
-  auto store_row = [&](bf16_t* row, const f32x16 (&acc)[NO], float scale) {
+  // Buffer stores through a descriptor whose extent ends with row T - 1: every lane stores (rows
+  // past T are dropped by the range check), no per-lane branch.
+  auto store_row = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t voff, const f32x16 (&acc)[NO], float scale) {
 #pragma unroll
     for (int n = 0; n < NO; ++n)
 #pragma unroll
@@ -1150,7 +1166,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
         const uint32_t y0 = pack2(c[8 * k + 4] * scale, c[8 * k + 5] * scale), y1 = pack2(c[8 * k + 6] * scale, c[8 * k + 7] * scale);
         const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
         const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
-        *reinterpret_cast<uint4*>(row + n * 32 + 16 * k + 8 * h32) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{s0[0], s1[0], s0[1], s1[1]}, rs,
+                                               voff + (uint32_t)((n * 32 + 16 * k) * 2), 0, 0);
       }
   };
   for (;;) {
@@ -1168,12 +1185,15 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
   // the next item's K / V (the dS^T image is free: the last tile's dQ products are behind its
   // final barrier), under this epilogue's stores
   if (has_next) dma_kv(nb, nhh, nkb0);
+  {
+    const uint64_t org = ((uint64_t)b * a.T + kb0) * ld * 2;  // row kb0 of this sequence
+    const __amdgpu_buffer_rsrc_t rso =
+        kv_rsrc(a.dqkv, org + (uint64_t)(a.T - kb0) * ld * 2, org);  // extent: through row T - 1
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    if (mykey[g] < a.T) {  // the same for both lanes of a row: the swaps pair active lanes only
-      bf16_t* krow = a.dqkv + ((long)b * a.T + mykey[g]) * ld + a.D + hh * 64;
-      store_row(krow, dk[g], sc);
-      store_row(krow + a.D, dv[g], vs);
+    for (int g = 0; g < 2; ++g) {
+      const uint32_t voff = (uint32_t)(((64 * w + 32 * g + l32) * ld + a.D + hh * 64 + 8 * h32) * 2);
+      store_row(rso, voff, dk[g], sc);
+      store_row(rso, voff + (uint32_t)(a.D * 2), dv[g], vs);
     }
   }
   if (a.dbias) {
@@ -1210,9 +1230,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
       atomicAdd(a.dbias + (1 + tk) * a.D + hh * 64 + d, s);
     }
   }
-  // the item after the next one (its atomic's latency under this epilogue's stores); read after
-  // the next item's prologue barrier
-  if (threadIdx.x == 0 && has_next) *sItem = atomicAdd(a.work, 1) + (int)gridDim.x;
+  // the item after the next one; read after the next item's prologue barrier
+  if (threadIdx.x == 0 && has_next) *sItem = nn_raw + (int)gridDim.x;
   BWD64_PE(3);
   if (!has_next) break;
   ++bwd64_it;
@@ -1222,6 +1241,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd64_kernel(const AttnArgs a) {
   item = nxt;
   setup(item);
   zero_acc();
+  // K / V landed (and this item's stores drained).  Waiting for the DMA alone -- vmcnt(16), the
+  // 16 dK / dV stores being younger -- took the transition from 6.3k to 4.0k cycles but measured
+  // no faster per kernel (profiles/round6_attn_bwd64_transition_ab.txt), so the count-free wait stays.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   convert_kv();
