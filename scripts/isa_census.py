@@ -68,7 +68,9 @@ def main():
     lab = {l.split(":")[0].strip(): i for i, l in enumerate(body) if re.match(r"^\.LBB\w+:", l.strip())}
     start, end = hdr, hdr
     nxt = min([h for h in hdrs if h > hdr] + [len(body)])
-    prev = max([h for h in hdrs if h < hdr] + [0])  # back edges of an enclosing loop jump before it
+    # back edges of an enclosing (or earlier) loop jump to or before the nearest loop header ahead of it
+    allh = [i for i, l in enumerate(body) if "Loop Header" in l]
+    prev = max([h for h in allh if h < hdr] + [-1])
     for i, l in enumerate(body[:nxt]):
         mm = re.search(r"s_c?branch\w*\s+(\.LBB\w+)", l)
         if mm and i > hdr and prev < lab.get(mm.group(1), 1 << 30) <= hdr:
