@@ -96,6 +96,11 @@ __global__ __launch_bounds__(256) void sumsq_chunks_kernel(const int64_t* __rest
   if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
+#ifndef MG_ADAMW_U
+#define MG_ADAMW_U 2
+#endif
+constexpr int kAdamwU = MG_ADAMW_U;  // float4 groups per thread per iteration: 1 / 4 measured no faster (PERF.md)
+
 // chunk b updates master/param/grad[chunk_start[b] ...] and the moments at
 // m/v[moment_start[b] ...] (moment_start == nullptr: the same index).  Replicated DP keeps
 // moments for the whole flat buffer; ZeRO-1 keeps them only for the rank's pieces, packed.
@@ -128,7 +133,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(
   const int len = chunk_len[c];
   const float decay = 1.f - lr * chunk_wd[c];
   // every operand is touched once per step: non-temporal loads / stores (no L2 / MALL pollution),
-  // and two float4 groups per thread per iteration so 8 loads are in flight before any use
+  // and kAdamwU float4 groups per thread per iteration so 4 kAdamwU loads are in flight before any use
   auto upd = [&](float (&pa)[4], const float (&ga)[4], float (&ma)[4], float (&va)[4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -139,10 +144,10 @@ __global__ __launch_bounds__(256) void adamw_kernel(
     }
   };
   int i = threadIdx.x * 4;
-  for (; i + 1024 + 4 <= len; i += 2048) {
-    float pa[2][4], ga[2][4], ma[2][4], va[2][4];
+  for (; i + (kAdamwU - 1) * 1024 + 4 <= len; i += kAdamwU * 1024) {
+    float pa[kAdamwU][4], ga[kAdamwU][4], ma[kAdamwU][4], va[kAdamwU][4];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < kAdamwU; ++u) {
       const long e = s0 + i + u * 1024, me = ms0 + i + u * 1024;
       ld4_nt(master + e, pa[u]);
       load_grad4(grad, e, ga[u]);
@@ -150,7 +155,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(
       ld4_nt(v + me, va[u]);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < kAdamwU; ++u) {
       const long e = s0 + i + u * 1024, me = ms0 + i + u * 1024;
       upd(pa[u], ga[u], ma[u], va[u]);
       if (zg) st4_nt(zg + e, z4);  // after the grad's use: its load has returned
